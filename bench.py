@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Msamples/s of the SDF path-trace hot path.
+
+Workload (BASELINE.json configs[2], the metric's "1920x1080x8-bounce"): the
+32-node sdf_editor graph (scenes.c3_graph32), 1920x1080, 8 bounces, progressive
+accumulation, 256 spp per render.  One *step* = one pt_dispatch of ``--spp``
+(default 16) frames per pixel over this rank's tiles; 16 steps = the 256-spp
+render.  Inputs (scene tables, image) are resident in HBM before timing.
+
+Multi-GPU (``torchrun --nproc-per-node N``): cyclic 8x8-tile ownership, each
+rank renders its 1/N of the tiles for N*spp frames per step (weak scaling:
+fixed samples per GPU), and the step ends with the RCCL sum-reduce of the
+accumulation image onto rank 0 (bit-identical to a 1-GPU render).
+
+Prints ONE JSON line (rank 0).  See DESIGN.md 5 for the roofline accounting.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Msamples/sec at 1920×1080×8-bounce; achieved HBM GB/s vs gfx950 peak"
+PEAK_F32_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (vector), spec
+PEAK_F32_TFLOPS_NONPACKED = 78.6
+PEAK_HBM_GBS = 8000.0  # spec
+
+# Algorithmic flop weights per counted event; FMA = 2,
+# sqrt/sin/cos excluded (counted as transcendentals).
+W_XFORM = 54
+W_SDF = {"sdf_sphere": 7, "sdf_cube": 19, "sdf_torus": 11, "sdf_octahedron": 22}
+W_FINALISE = 1
+W_COMB = {"comb_union": 1, "comb_sub": 3, "comb_assign": 0}
+W_MARCH = 10
+W_NORMAL = 29  # per calc_normal (6 maps counted separately)
+W_AABB = 40
+W_SHADE = 100
+W_CAMERA = 25
+W_ACCUM = 10
+
+
+def algorithmic_flops(st: dict) -> float:
+    xf = st["xform_union"] + st["xform_shape"]
+    f = W_XFORM * xf + W_FINALISE * xf
+    f += sum(w * st[k] for k, w in W_SDF.items())
+    f += sum(w * st[k] for k, w in W_COMB.items())
+    f += W_MARCH * st["march_steps"] + W_NORMAL * (st["normal_maps"] // 6) + W_AABB * st["aabb_tests"]
+    f += W_SHADE * st["shaded"] + (W_CAMERA + W_ACCUM) * st["samples"]
+    return float(f)
+
+
+def cpu_baseline(scene, w, h, bounces, threads: int, row_stride: int, spp: int) -> dict:
+    from oracle import oracle as O  # test infrastructure: the CPU restatement
+
+    osc = O.OracleScene(scene.rows())
+    c = O.Constants(0.0, 1, float(np.float32(w) / np.float32(h)), 1)
+    s = O.Settings(0, bounces, 1.0, 1.0, 0)
+    osc.render(w, h, c, s, 1, row_stride=row_stride * 8, threads=threads)  # warm caches
+    t0 = time.perf_counter()
+    osc.render(w, h, c, s, spp, row_stride=row_stride, threads=threads)
+    dt = time.perf_counter() - t0
+    rows = len(range(0, h, row_stride))
+    samples = rows * w * spp
+    return {"value": samples / dt / 1e6, "unit": "Msamples/sec", "cores": threads, "kind": "port",
+            "sample": f"C oracle (oracle/pt_oracle.c, -O3, {threads} threads) on every {row_stride}th row of the "
+                      f"same {w}x{h} 8-bounce c3 frame, {spp} spp ({samples} samples, {dt:.1f} s)"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--spp", type=int, default=16, help="frames per pixel per step (per GPU-share)")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--scene", default="c3")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-row-stride", type=int, default=8)
+    ap.add_argument("--cpu-spp", type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_
+
+        dist = dist_
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from compute_path_tracer_amd import _native as N
+    from compute_path_tracer_amd import scenes
+    from compute_path_tracer_amd.path_tracer import PathTracer
+    from compute_path_tracer_amd.sdf_editor import CompData
+
+    ed = scenes.SCENES[args.scene]()
+    prog = ed.compile(CompData())
+    settings = N.Settings(debug=0, bounces=args.bounces, scale=1.0, fov=1.0, aabb=0)
+    pt = PathTracer(args.width, args.height, prog, device=local_rank, settings=settings)
+    aspect = float(np.float32(args.width) / np.float32(args.height))
+    spp_step = args.spp * world  # weak scaling: each rank owns 1/world of the tiles
+    if world > 1:
+        pt.set_tiles(rank, world)
+        uid = [pt.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        pt.comm_init(world, rank, uid[0])
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    frame = [1]
+
+    def step():
+        c = N.Constants(time=0.0, frame=frame[0], aspect=aspect, last_clear=frame[0])
+        pt.dispatch(c, spp_step)
+        frame[0] += spp_step
+        if world > 1:
+            pt.reduce(0)
+
+    # algorithmic work per step from the instrumented kernel (outside timing)
+    st = pt.stats(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), spp_step)
+
+    for _ in range(args.warmup):
+        step()
+    pt.sync()
+    barrier()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        if world == 1:
+            kernel_ms.append(pt.last_dispatch_ms())
+    pt.sync()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if world > 1:
+        # per-launch kernel time on this rank (events on the library stream)
+        pt.dispatch(N.Constants(time=0.0, frame=frame[0], aspect=aspect, last_clear=frame[0]), spp_step)
+        kernel_ms.append(pt.last_dispatch_ms())
+
+    pixels = args.width * args.height
+    samples_step = pixels * args.spp * world  # all ranks
+    value = samples_step * args.steps / dt / 1e6
+    ms_step = dt * 1e3 / args.steps
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    k_ms = float(np.mean(kernel_ms))
+    flops_per_launch = algorithmic_flops(st)
+    rank_pixels = st["samples"] / max(1, spp_step)
+    bytes_per_launch = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per launch
+    achieved_tf = flops_per_launch / (k_ms * 1e-3) / 1e12
+    achieved_gbs = bytes_per_launch / (k_ms * 1e-3) / 1e9
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Msamples/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (scenes.c3_graph32: 32-node sdf_editor graph, seed 42)",
+        "config": {"workload": f"{args.scene} {args.width}x{args.height}, {args.bounces} bounces, "
+                               f"{args.spp * world} spp per step ({args.spp} per GPU-share), progressive accumulate",
+                   "width": args.width, "height": args.height, "bounces": args.bounces,
+                   "spp_per_step": args.spp * world, "parallelism": f"tiles{world}"},
+        "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_TFLOPS, 4), "traffic": None,
+                     "algorithmic_flops_per_sample": round(flops_per_launch / max(1, st["samples"]), 1),
+                     "frac_nonpacked": round(achieved_tf / PEAK_F32_TFLOPS_NONPACKED, 4),
+                     "kernel_ms_per_launch": round(k_ms, 3)},
+        "hbm": {"achieved": round(achieved_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "algorithmic_bytes_per_launch": bytes_per_launch},
+        "work": st,
+    }
+    if not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(ed, args.width, args.height, args.bounces, args.cpu_threads,
+                                           args.cpu_row_stride, args.cpu_spp)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,89 @@
+// pt_math.h -- f32 helpers shared by the HIP kernel and the host-side scene
+// derivation in pt_runtime.hip.  Compiled with -ffp-contract=off on both
+// sides: every fused multiply-add is an explicit fmaf.
+//
+// The GLSL builtins' precision is left to the driver by the spec (naga +
+// vendor driver upstream, parity unpinned there); this file is the semantics
+// contract of DESIGN.md section 3 that makes host and device agree bitwise.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#define PT_HD __host__ __device__ __forceinline__
+
+// GLSL 4.50 8.3: min(x, y) = y < x ? y : x;  max(x, y) = x < y ? y : x.
+PT_HD float pt_gmin(float x, float y) { return (y < x) ? y : x; }
+PT_HD float pt_gmax(float x, float y) { return (x < y) ? y : x; }
+
+// rng.glsl:1-9
+PT_HD uint32_t pt_wang_hash(uint32_t &seed) {
+    seed = (seed ^ 61u) ^ (seed >> 16);
+    seed *= 9u;
+    seed = seed ^ (seed >> 4);
+    seed *= 0x27d4eb2du;
+    seed = seed ^ (seed >> 15);
+    return seed;
+}
+// rng.glsl:11-14: float(u) / 2^32 (exact scaling of the RN conversion)
+PT_HD float pt_random01(uint32_t &state) { return float(pt_wang_hash(state)) * 2.3283064365386963e-10f; }
+
+// rng.glsl:26-36
+PT_HD uint32_t pt_gen_rng(int32_t x, int32_t y, int32_t frame, int32_t w, int32_t h) {
+    uint32_t a = uint32_t((float(x) * 0.5f + 0.5f) * float(w));
+    uint32_t b = uint32_t((float(y) * 0.5f + 0.5f) * float(h));
+    return (a * 1973u + b * 9277u + uint32_t(frame) * 26699u) | 1u;
+}
+
+// sin/cos contract: Cody-Waite reduction by pi/2 + minimax polynomials on
+// [-pi/4, pi/4]; identical to oracle/pt_oracle.c:sincos_q.
+PT_HD float pt_sin_poly(float r) {
+    float s = r * r;
+    float p = fmaf(s, -1.9515295891e-4f, 8.3321608736e-3f);
+    p = fmaf(s, p, -1.6666654611e-1f);
+    return fmaf(r * s, p, r);
+}
+PT_HD float pt_cos_poly(float r) {
+    float s = r * r;
+    float p = fmaf(s, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    p = fmaf(s, p, 4.166664568298827e-2f);
+    float t = fmaf(s, p, -0.5f);
+    return fmaf(s, t, 1.0f);
+}
+// Reduced argument and quadrant of x (|x| <= 2^24; callers map the rest to NaN).
+PT_HD float pt_reduce(float x, int &q) {
+    float k = rintf(x * 0.63661977236758134f);
+    float r = fmaf(-k, 1.5703125f, x);
+    r = fmaf(-k, 4.837512969970703125e-4f, r);
+    r = fmaf(-k, 7.549789954891882e-8f, r);
+    q = int(k);
+    return r;
+}
+PT_HD void pt_sincos(float x, float &s, float &c) {
+    if (!(fabsf(x) <= 16777216.0f)) {
+        s = c = (x - x) / (x - x);
+        return;
+    }
+    int q;
+    float r = pt_reduce(x, q);
+    float sp = pt_sin_poly(r), cp = pt_cos_poly(r);
+    switch (q & 3) {
+        case 0: s = sp; c = cp; break;
+        case 1: s = cp; c = -sp; break;
+        case 2: s = -sp; c = -cp; break;
+        default: s = -cp; c = sp; break;
+    }
+}
+
+struct pt_f3 {
+    float x, y, z;
+};
+PT_HD float pt_dot(pt_f3 a, pt_f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PT_HD float pt_length(pt_f3 a) { return sqrtf(pt_dot(a, a)); }
+// GLSL normalize(v) = v / length(v)
+PT_HD pt_f3 pt_normalize(pt_f3 a) {
+    float l = pt_length(a);
+    return pt_f3{a.x / l, a.y / l, a.z / l};
+}

@@ -1,0 +1,499 @@
+// pt_runtime.hip -- implementation of the C ABI in include/pt_abi.h.
+//
+// Owns what the reference's wgpu objects owned (path_tracer.rs:18-163,
+// structs.rs:113-184, primitives.rs:59-157): the RGBA32F accumulation image,
+// the scene program and its parameter buffer, and the dispatch.  One HIP
+// stream per context; RCCL communicator for the multi-GPU image reduce.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/pt_abi.h"
+#include "pt_device.h"
+#include "pt_math.h"
+
+void pt_launch_render(const PtLaunch &L, bool stats, hipStream_t stream);
+
+static_assert(sizeof(pt_constants) == 16, "Constants is 16 B (path_tracer.rs:149-155)");
+static_assert(sizeof(pt_settings) == 20, "Settings is 20 B (path_tracer.rs:157-163)");
+static_assert(sizeof(pt_op) == 33 * 4, "pt_op layout");
+static_assert(sizeof(pt_aabb) == 14 * 4, "pt_aabb layout");
+static_assert(sizeof(pt_scene_node) == 33 * 4, "pt_scene_node layout");
+static_assert(PT_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "RCCL unique id size");
+
+struct pt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t width = 0, height = 0;
+    float *accum = nullptr;
+    float *reduced = nullptr;
+    // program
+    std::vector<pt_op> ops;
+    std::vector<pt_aabb> aabbs;
+    uint32_t n_check = 1;
+    bool have_program = false, have_data = false;
+    uint32_t n_data_expected = 0;
+    // device tables
+    PtNode *d_nodes = nullptr;
+    PtAabb *d_aabbs = nullptr;
+    PtMat *d_mats = nullptr;
+    size_t cap_nodes = 0, cap_aabbs = 0, cap_mats = 0;
+    unsigned long long *d_stats = nullptr;
+    // tiles
+    uint32_t rank = 0, nranks = 1;
+    ncclComm_t comm = nullptr;
+    uint32_t comm_nranks = 0;
+    // timing
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string err;
+};
+
+namespace {
+
+int fail(pt_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                      \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(ctx, PT_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_));     \
+    } while (0)
+
+int ensure(pt_ctx *c, void **ptr, size_t &cap, size_t need) {
+    if (need <= cap && *ptr) return PT_OK;
+    if (*ptr) HIPCHK(c, hipFree(*ptr));
+    *ptr = nullptr;
+    size_t bytes = std::max<size_t>(need, 1);
+    HIPCHK(c, hipMalloc(ptr, bytes));
+    cap = bytes;
+    return PT_OK;
+}
+
+int alloc_image(pt_ctx *c, uint32_t w, uint32_t h) {
+    if (c->accum) HIPCHK(c, hipFree(c->accum));
+    if (c->reduced) HIPCHK(c, hipFree(c->reduced));
+    c->accum = c->reduced = nullptr;
+    c->width = w;
+    c->height = h;
+    size_t bytes = size_t(w) * size_t(h) * 16;
+    HIPCHK(c, hipMalloc(&c->accum, std::max<size_t>(bytes, 16)));
+    HIPCHK(c, hipMemsetAsync(c->accum, 0, std::max<size_t>(bytes, 16), c->stream));
+    return PT_OK;
+}
+
+// Host expansion of (program, data[]) into the device tables.  Every value is
+// the f32 expression the generated GLSL evaluates on the GPU, evaluated here
+// once with the same rounding (see pt_device.h).
+int derive(pt_ctx *c, const float *data, uint32_t n, std::vector<PtNode> &nodes, std::vector<PtAabb> &boxes,
+           std::vector<PtMat> &mats) {
+    auto in = [&](uint32_t s) { return s < n; };
+    nodes.resize(c->ops.size());
+    mats.clear();
+    PtMat mdef;
+    std::memset(&mdef, 0, sizeof mdef);
+    {
+        pt_f3 z{0.0f, 0.0f, 0.0f};
+        pt_f3 nl = pt_normalize(z);  // MDEF light = vec3(0): normalize -> NaN, as upstream
+        mdef.emis[0] = nl.x * 0.0f;
+        mdef.emis[1] = nl.y * 0.0f;
+        mdef.emis[2] = nl.z * 0.0f;
+    }
+    mats.push_back(mdef);
+    for (size_t i = 0; i < c->ops.size(); ++i) {
+        const pt_op &op = c->ops[i];
+        PtNode &d = nodes[i];
+        std::memset(&d, 0, sizeof d);
+        d.op = int32_t(op.opcode);
+        d.shape = int32_t(op.shape);
+        d.combine = int32_t(op.combine);
+        d.check = op.check;
+        if (!in(op.scale)) return fail(c, PT_ERR_INVALID, "op references data slot out of range");
+        for (int k = 0; k < 3; ++k)
+            if (!in(op.position[k]) || !in(op.rotation[k]))
+                return fail(c, PT_ERR_INVALID, "op references data slot out of range");
+        const float s = data[op.scale];
+        const float inv = 1.0f / s;  // `1.0 / data[scale]`
+        d.inv = inv;
+        for (int k = 0; k < 3; ++k) d.m[k] = data[op.position[k]] * inv;  // pos * (1.0 / s)
+        uint32_t f = 0;
+        if (inv != 1.0f) f |= PT_NF_SCALE;
+        if (d.m[0] != 0.0f || d.m[1] != 0.0f || d.m[2] != 0.0f) f |= PT_NF_POS;
+        pt_sincos(data[op.rotation[0]], d.sx, d.cx);
+        pt_sincos(data[op.rotation[1]], d.sy, d.cy);
+        pt_sincos(data[op.rotation[2]], d.sz, d.cz);
+        if (!(d.cx == 1.0f && d.sx == 0.0f)) f |= PT_NF_RX;
+        if (!(d.cy == 1.0f && d.sy == 0.0f)) f |= PT_NF_RY;
+        if (!(d.cz == 1.0f && d.sz == 0.0f)) f |= PT_NF_RZ;
+        d.flags = f;
+        if (op.opcode == PT_OP_SHAPE) {
+            for (int k = 0; k < 3; ++k) {
+                if (!in(op.size[k])) return fail(c, PT_ERR_INVALID, "size slot out of range");
+                d.size[k] = data[op.size[k]];
+            }
+            for (int k = 0; k < 18; ++k)
+                if (!in(op.material[k])) return fail(c, PT_ERR_INVALID, "material slot out of range");
+            const uint32_t *ms = op.material;
+            PtMat m;
+            std::memset(&m, 0, sizeof m);
+            for (int k = 0; k < 3; ++k) {
+                m.col[k] = data[ms[k]];
+                m.spec_col[k] = data[ms[8 + k]];
+            }
+            m.spec = data[ms[7]];
+            m.rough2 = data[ms[11]] * data[ms[11]];
+            pt_f3 nl = pt_normalize(pt_f3{data[ms[4]], data[ms[5]], data[ms[6]]});
+            const float br = data[ms[3]];
+            m.emis[0] = nl.x * br;
+            m.emis[1] = nl.y * br;
+            m.emis[2] = nl.z * br;
+            d.mat = int32_t(mats.size());
+            mats.push_back(m);
+        }
+    }
+    boxes.resize(c->aabbs.size());
+    for (size_t i = 0; i < c->aabbs.size(); ++i) {
+        const pt_aabb &a = c->aabbs[i];
+        for (int k = 0; k < 3; ++k)
+            if (!in(a.union_position[k]) || !in(a.shape_position[k]) || !in(a.size[k]))
+                return fail(c, PT_ERR_INVALID, "aabb slot out of range");
+        if (!in(a.union_scale) || !in(a.shape_scale) || !in(a.aabb_exaggeration))
+            return fail(c, PT_ERR_INVALID, "aabb slot out of range");
+        float so[3];
+        switch (a.so_kind) {
+            case PT_SO_SCALAR: so[0] = so[1] = so[2] = data[a.size[0]]; break;
+            case PT_SO_VEC3:
+                for (int k = 0; k < 3; ++k) so[k] = data[a.size[k]];
+                break;
+            case PT_SO_TORUS: {
+                const float R = data[a.size[0]], r = data[a.size[1]];
+                so[0] = R + r;
+                so[1] = r;
+                so[2] = R + r;
+                break;
+            }
+            default: so[0] = so[1] = so[2] = 1.0f; break;
+        }
+        const float sc = data[a.union_scale] * data[a.shape_scale];
+        const float ex = data[a.aabb_exaggeration];
+        PtAabb &b = boxes[i];
+        std::memset(&b, 0, sizeof b);
+        for (int k = 0; k < 3; ++k) {
+            const float ctr = data[a.union_position[k]] + data[a.shape_position[k]];
+            const float hs = (so[k] * sc) * ex;
+            b.bmin[k] = ctr - hs;  // from_pos_size (aabb.glsl:13-19)
+            b.bmax[k] = ctr + hs;
+        }
+        b.back = a.back;
+    }
+    return PT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pt_abi_version(void) { return PT_ABI_VERSION; }
+
+int pt_create(int hip_device, uint32_t width, uint32_t height, pt_ctx **out) {
+    if (!out) return PT_ERR_INVALID;
+    *out = nullptr;
+    pt_ctx *c = new (std::nothrow) pt_ctx();
+    if (!c) return PT_ERR_INVALID;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0 || hip_device < 0 || hip_device >= ndev) {
+        delete c;
+        return PT_ERR_HIP;
+    }
+    c->device = hip_device;
+    if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc(&c->d_stats, sizeof(unsigned long long) * PT_ST_COUNT) != hipSuccess) {
+        pt_destroy(c);
+        return PT_ERR_HIP;
+    }
+    if (alloc_image(c, width, height) != PT_OK) {
+        pt_destroy(c);
+        return PT_ERR_HIP;
+    }
+    *out = c;
+    return PT_OK;
+}
+
+int pt_resize_clear(pt_ctx *c, uint32_t width, uint32_t height) {
+    if (!c) return PT_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (width == c->width && height == c->height) {
+        HIPCHK(c, hipMemsetAsync(c->accum, 0, std::max<size_t>(size_t(width) * height * 16, 16), c->stream));
+        return PT_OK;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return alloc_image(c, width, height);
+}
+
+int pt_set_program(pt_ctx *c, const pt_op *ops, uint32_t n_ops, const pt_aabb *aabbs, uint32_t n_aabb,
+                   uint32_t n_check) {
+    if (!c) return PT_ERR_INVALID;
+    if ((n_ops && !ops) || (n_aabb && !aabbs)) return fail(c, PT_ERR_INVALID, "null program arrays");
+    if (n_check > PT_MAX_CHECK) return fail(c, PT_ERR_UNSUPPORTED, "more than 128 check[] entries");
+    int depth = 0, max_depth = 0;
+    for (uint32_t i = 0; i < n_ops; ++i) {
+        const pt_op &o = ops[i];
+        if (o.opcode == PT_OP_UNION_BEGIN) {
+            max_depth = std::max(max_depth, ++depth);
+        } else if (o.opcode == PT_OP_UNION_END) {
+            if (--depth < 0) return fail(c, PT_ERR_INVALID, "unbalanced UNION_END");
+            if (o.combine != PT_COMBINE_UNION && o.combine != PT_COMBINE_SUBTRACTION)
+                return fail(c, PT_ERR_INVALID, "UNION_END combine must be union/subtraction");
+        } else if (o.opcode == PT_OP_SHAPE) {
+            if (depth < 1) return fail(c, PT_ERR_INVALID, "shape outside a union");
+            if (o.shape == PT_NODE_PLANE) return fail(c, PT_ERR_UNSUPPORTED, "Shapes::Plane is not implemented upstream");
+            if (o.shape < PT_NODE_SPHERE || o.shape > PT_NODE_OCTAHEDRON) return fail(c, PT_ERR_INVALID, "bad shape");
+            if (o.combine > PT_COMBINE_SUBTRACTION) return fail(c, PT_ERR_INVALID, "bad combine");
+            if (o.check >= int32_t(n_check)) return fail(c, PT_ERR_INVALID, "check index out of range");
+        } else {
+            return fail(c, PT_ERR_INVALID, "bad opcode");
+        }
+    }
+    if (depth != 0) return fail(c, PT_ERR_INVALID, "unbalanced UNION_BEGIN");
+    if (max_depth > PT_MAX_DEPTH) return fail(c, PT_ERR_UNSUPPORTED, "union nesting deeper than 8");
+    for (uint32_t i = 0; i < n_aabb; ++i)
+        if (aabbs[i].back < 0 || aabbs[i].back >= int32_t(n_check) || aabbs[i].so_kind > PT_SO_TORUS)
+            return fail(c, PT_ERR_INVALID, "bad aabb record");
+    c->ops.assign(ops, ops + n_ops);
+    c->aabbs.assign(aabbs, aabbs + n_aabb);
+    c->n_check = n_check;
+    c->have_program = true;
+    c->have_data = false;  // queue_compile reallocates data[] (sdf_editor.rs:36-40)
+    return PT_OK;
+}
+
+int pt_set_data(pt_ctx *c, const float *data, uint32_t n) {
+    if (!c) return PT_ERR_INVALID;
+    if (!c->have_program) return fail(c, PT_ERR_STATE, "pt_set_data before pt_set_program");
+    if (n && !data) return fail(c, PT_ERR_INVALID, "null data");
+    std::vector<PtNode> nodes;
+    std::vector<PtAabb> boxes;
+    std::vector<PtMat> mats;
+    int rc = derive(c, data, n, nodes, boxes, mats);
+    if (rc != PT_OK) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    // stream-ordered upload: in-flight dispatches finish with the old tables
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((rc = ensure(c, reinterpret_cast<void **>(&c->d_nodes), c->cap_nodes, nodes.size() * sizeof(PtNode))) != PT_OK)
+        return rc;
+    if ((rc = ensure(c, reinterpret_cast<void **>(&c->d_aabbs), c->cap_aabbs, boxes.size() * sizeof(PtAabb))) != PT_OK)
+        return rc;
+    if ((rc = ensure(c, reinterpret_cast<void **>(&c->d_mats), c->cap_mats, mats.size() * sizeof(PtMat))) != PT_OK)
+        return rc;
+    if (!nodes.empty())
+        HIPCHK(c, hipMemcpyAsync(c->d_nodes, nodes.data(), nodes.size() * sizeof(PtNode), hipMemcpyHostToDevice, c->stream));
+    if (!boxes.empty())
+        HIPCHK(c, hipMemcpyAsync(c->d_aabbs, boxes.data(), boxes.size() * sizeof(PtAabb), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_mats, mats.data(), mats.size() * sizeof(PtMat), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->have_data = true;
+    return PT_OK;
+}
+
+int pt_set_tiles(pt_ctx *c, uint32_t rank, uint32_t nranks) {
+    if (!c) return PT_ERR_INVALID;
+    if (nranks == 0 || rank >= nranks) return fail(c, PT_ERR_INVALID, "rank must be < nranks");
+    c->rank = rank;
+    c->nranks = nranks;
+    return pt_resize_clear(c, c->width, c->height);
+}
+
+static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t spp, PtLaunch &L) {
+    if (!c) return PT_ERR_INVALID;
+    if (!k || !s) return fail(c, PT_ERR_INVALID, "null constants/settings");
+    if (!c->have_program || !c->have_data) return fail(c, PT_ERR_STATE, "no program/data uploaded");
+    if (s->bounces < 0) return fail(c, PT_ERR_INVALID, "negative bounces");
+    std::memset(&L, 0, sizeof L);
+    L.nodes = c->d_nodes;
+    L.aabbs = c->d_aabbs;
+    L.mats = c->d_mats;
+    L.accum = c->accum;
+    L.n_nodes = int32_t(c->ops.size());
+    L.n_aabb = int32_t(c->aabbs.size());
+    L.width = int32_t(c->width);
+    L.height = int32_t(c->height);
+    L.tiles_x = int32_t((c->width + PT_TILE - 1) / PT_TILE);
+    const int64_t tiles = int64_t(L.tiles_x) * int64_t((c->height + PT_TILE - 1) / PT_TILE);
+    L.n_tiles = int32_t(tiles > int64_t(c->rank) ? (tiles - int64_t(c->rank) + c->nranks - 1) / c->nranks : 0);
+    L.rank = int32_t(c->rank);
+    L.nranks = int32_t(c->nranks);
+    L.frame0 = k->frame;
+    L.last_clear0 = k->last_clear;
+    L.spp = int32_t(spp);
+    L.debug = s->debug;
+    L.bounces = s->bounces;
+    L.fov = s->fov;
+    L.aspect = k->aspect;
+    L.write = 1;
+    return PT_OK;
+}
+
+int pt_dispatch(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t spp) {
+    PtLaunch L;
+    int rc = make_launch(c, k, s, spp, L);
+    if (rc != PT_OK) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    if (spp > 0 && L.n_tiles > 0) {
+        // bound a single launch's length; chunks continue frame/last_clear
+        const uint32_t chunk = 64;
+        for (uint32_t done = 0; done < spp; done += chunk) {
+            PtLaunch Lc = L;
+            Lc.spp = int32_t(std::min(chunk, spp - done));
+            Lc.frame0 = int32_t(uint32_t(L.frame0) + done);
+            Lc.last_clear0 = int32_t(uint32_t(L.last_clear0) + done);
+            if (L.debug != 0 && done + chunk < spp) continue;  // direct stores: only the last frame survives
+            pt_launch_render(Lc, false, c->stream);
+            HIPCHK(c, hipGetLastError());
+        }
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return PT_OK;
+}
+
+int pt_dispatch_stats(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t spp,
+                      uint64_t counters[PT_STAT_COUNT]) {
+    static_assert(PT_STAT_COUNT == PT_ST_COUNT, "stat count");
+    PtLaunch L;
+    int rc = make_launch(c, k, s, spp, L);
+    if (rc != PT_OK) return rc;
+    if (!counters) return fail(c, PT_ERR_INVALID, "null counters");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * PT_ST_COUNT, c->stream));
+    L.stats = c->d_stats;
+    L.write = 0;
+    if (spp > 0 && L.n_tiles > 0) {
+        pt_launch_render(L, true, c->stream);
+        HIPCHK(c, hipGetLastError());
+    }
+    unsigned long long host[PT_ST_COUNT];
+    HIPCHK(c, hipMemcpyAsync(host, c->d_stats, sizeof host, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < PT_ST_COUNT; ++i) counters[i] = host[i];
+    return PT_OK;
+}
+
+int pt_read_accum(pt_ctx *c, float *rgba, size_t bytes) {
+    if (!c) return PT_ERR_INVALID;
+    const size_t need = size_t(c->width) * c->height * 16;
+    if (!rgba || bytes < need) return fail(c, PT_ERR_SIZE, "readback buffer too small");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(rgba, c->accum, need, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_accum_device_ptr(pt_ctx *c, void **dev_ptr, size_t *bytes) {
+    if (!c || !dev_ptr || !bytes) return PT_ERR_INVALID;
+    *dev_ptr = c->accum;
+    *bytes = size_t(c->width) * c->height * 16;
+    return PT_OK;
+}
+
+int pt_get_size(const pt_ctx *c, uint32_t *w, uint32_t *h) {
+    if (!c || !w || !h) return PT_ERR_INVALID;
+    *w = c->width;
+    *h = c->height;
+    return PT_OK;
+}
+
+int pt_comm_get_unique_id(uint8_t id[PT_COMM_ID_BYTES]) {
+    if (!id) return PT_ERR_INVALID;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return PT_ERR_RCCL;
+    std::memcpy(id, u.internal, PT_COMM_ID_BYTES);
+    return PT_OK;
+}
+
+int pt_comm_init(pt_ctx *c, uint32_t nranks, uint32_t rank, const uint8_t id[PT_COMM_ID_BYTES]) {
+    if (!c || !id || nranks == 0 || rank >= nranks) return fail(c, PT_ERR_INVALID, "bad communicator arguments");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->comm) {
+        ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+    }
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, PT_COMM_ID_BYTES);
+    ncclResult_t r = ncclCommInitRank(&c->comm, int(nranks), u, int(rank));
+    if (r != ncclSuccess) return fail(c, PT_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    c->comm_nranks = nranks;
+    return PT_OK;
+}
+
+int pt_reduce_accum(pt_ctx *c, int root) {
+    if (!c) return PT_ERR_INVALID;
+    if (!c->comm) return fail(c, PT_ERR_STATE, "pt_comm_init not called");
+    if (root < 0 || uint32_t(root) >= c->comm_nranks) return fail(c, PT_ERR_INVALID, "bad root");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t count = size_t(c->width) * c->height * 4;
+    if (!c->reduced) HIPCHK(c, hipMalloc(&c->reduced, std::max<size_t>(count * 4, 16)));
+    // non-owned texels are exactly 0 on every other rank, so the sum is the
+    // bit-exact single-GPU image (x + 0 = x)
+    ncclResult_t r = ncclReduce(c->accum, c->reduced, count, ncclFloat32, ncclSum, root, c->comm, c->stream);
+    if (r != ncclSuccess) return fail(c, PT_ERR_RCCL, std::string("ncclReduce: ") + ncclGetErrorString(r));
+    return PT_OK;
+}
+
+int pt_read_reduced(pt_ctx *c, float *rgba, size_t bytes) {
+    if (!c) return PT_ERR_INVALID;
+    if (!c->reduced) return fail(c, PT_ERR_STATE, "no reduced image");
+    const size_t need = size_t(c->width) * c->height * 16;
+    if (!rgba || bytes < need) return fail(c, PT_ERR_SIZE, "readback buffer too small");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(rgba, c->reduced, need, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_sync(pt_ctx *c) {
+    if (!c) return PT_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_last_dispatch_ms(pt_ctx *c, float *ms) {
+    if (!c || !ms) return PT_ERR_INVALID;
+    if (!c->timed) return fail(c, PT_ERR_STATE, "no dispatch recorded");
+    HIPCHK(c, hipEventSynchronize(c->ev1));
+    HIPCHK(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return PT_OK;
+}
+
+const char *pt_last_error(const pt_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+void pt_destroy(pt_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    (void)hipFree(c->accum);
+    (void)hipFree(c->reduced);
+    (void)hipFree(c->d_nodes);
+    (void)hipFree(c->d_aabbs);
+    (void)hipFree(c->d_mats);
+    (void)hipFree(c->d_stats);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+}  // extern "C"

@@ -1,0 +1,187 @@
+"""Host mirror of the reference's ``PathTracer`` (src/path_tracer/path_tracer.rs).
+
+Same public surface -- ``new``/``remake_pipeline``/``update``/``compute_pass``,
+the ``Constants``/``Settings`` blocks with the reference defaults, the
+``changed`` flag -- but the wgpu pipeline, UBOs and storage texture are
+replaced by one native context (``include/pt_abi.h``) driving the HIP kernel.
+``render(spp)`` is the batched form: it is exactly ``spp`` repetitions of
+``update()`` + ``compute_pass()`` with no reset in between, executed as one
+launch that keeps the accumulation texel in registers.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+
+from . import _native as N
+from .sdf_editor import Program
+
+
+def default_settings() -> N.Settings:
+    """defaults_and_sliders_gui!(Settings, ...) (path_tracer.rs:157-163)."""
+    return N.Settings(debug=1, bounces=8, scale=1.0, fov=1.0, aabb=0)
+
+
+class PathTracer:
+    def __init__(self, width: int, height: int, program: Optional[Program] = None, data: Optional[np.ndarray] = None,
+                 device: int = 0, settings: Optional[N.Settings] = None):
+        """PathTracer::new (path_tracer.rs:28-60) + the storage texture it binds
+        (StorageTexturePackage::new, structs.rs:113-160).  ``width``/``height``
+        are the window size; the image is window * settings.scale."""
+        self._L = N.lib()
+        self.window = (int(width), int(height))
+        self.constants = N.Constants(time=0.0, frame=0, aspect=0.0, last_clear=0)
+        self.settings = settings if settings is not None else default_settings()
+        self.changed = False
+        self.device = device
+        self.size = self._scaled_size()
+        ctx = ctypes.c_void_p()
+        N.check("pt_create", self._L.pt_create(device, self.size[0], self.size[1], ctypes.byref(ctx)))
+        self._ctx = ctx
+        if program is not None:
+            self.remake_pipeline(program)
+            self.set_data(program.data if data is None else data)
+
+    # -- lifecycle -----------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._L.pt_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, fn: str, rc: int) -> None:
+        N.check(fn, rc, self._ctx)
+
+    def _scaled_size(self):
+        s = np.float32(self.settings.scale)
+        return (int(np.float32(self.window[0]) * s), int(np.float32(self.window[1]) * s))
+
+    # -- reference surface ---------------------------------------------------
+    def remake_pipeline(self, program: Program) -> None:
+        """path_tracer.rs:62-76: a topology change (queue_compile)."""
+        self._chk("pt_set_program", self._L.pt_set_program(self._ctx, program.ops, program.n_ops, program.aabbs,
+                                                            program.n_aabb, program.n_check))
+
+    def set_data(self, data: np.ndarray) -> None:
+        """DataArray::update (primitives.rs:131-151): value-only upload."""
+        arr = np.ascontiguousarray(data, dtype=np.float32)
+        self._chk("pt_set_data", self._L.pt_set_data(self._ctx, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                                      arr.size))
+
+    def update(self, resized: bool = False, reset: bool = False, time: float = 0.0,
+               window: Optional[tuple] = None) -> None:
+        """path_tracer.rs:97-118: reset on resize/settings change/Space, then
+        advance frame and last_clear."""
+        if window is not None:
+            self.window = (int(window[0]), int(window[1]))
+        if resized or self.changed or reset:
+            self.size = self._scaled_size()
+            self._chk("pt_resize_clear", self._L.pt_resize_clear(self._ctx, self.size[0], self.size[1]))
+            self.constants.last_clear = 0
+        self.constants.time = float(time)
+        self.constants.aspect = float(np.float32(self.window[0]) / np.float32(self.window[1]))  # setup.rs:84-86
+        self.constants.frame += 1
+        self.constants.last_clear += 1
+        self.changed = False
+
+    def compute_pass(self) -> None:
+        """path_tracer.rs:128-146: one frame (1 spp) with the current blocks."""
+        self._chk("pt_dispatch", self._L.pt_dispatch(self._ctx, ctypes.byref(self.constants),
+                                                      ctypes.byref(self.settings), 1))
+
+    # -- batched / multi-GPU ----------------------------------------------
+    def render(self, spp: int) -> None:
+        """``spp`` x (update(); compute_pass()) without resets, one dispatch."""
+        if spp <= 0:
+            return
+        if self.changed:
+            self.update()
+            self.constants.frame -= 1
+            self.constants.last_clear -= 1
+        c = N.Constants(time=self.constants.time, frame=self.constants.frame + 1,
+                        aspect=float(np.float32(self.window[0]) / np.float32(self.window[1])),
+                        last_clear=self.constants.last_clear + 1)
+        self.constants.aspect = c.aspect
+        self._chk("pt_dispatch", self._L.pt_dispatch(self._ctx, ctypes.byref(c), ctypes.byref(self.settings), spp))
+        self.constants.frame += spp
+        self.constants.last_clear += spp
+
+    def dispatch(self, constants: N.Constants, spp: int) -> None:
+        """Raw pt_dispatch with explicit constants (frame j = frame + j)."""
+        self._chk("pt_dispatch", self._L.pt_dispatch(self._ctx, ctypes.byref(constants), ctypes.byref(self.settings),
+                                                      spp))
+
+    def stats(self, constants: N.Constants, spp: int) -> dict:
+        buf = (ctypes.c_uint64 * N.PT_STAT_COUNT)()
+        self._chk("pt_dispatch_stats", self._L.pt_dispatch_stats(self._ctx, ctypes.byref(constants),
+                                                                  ctypes.byref(self.settings), spp, buf))
+        return dict(zip(N.STAT_NAMES, (int(v) for v in buf)))
+
+    def set_tiles(self, rank: int, nranks: int) -> None:
+        self._chk("pt_set_tiles", self._L.pt_set_tiles(self._ctx, rank, nranks))
+
+    def clear(self) -> None:
+        self._chk("pt_resize_clear", self._L.pt_resize_clear(self._ctx, self.size[0], self.size[1]))
+        self.constants.last_clear = 0
+
+    def sync(self) -> None:
+        self._chk("pt_sync", self._L.pt_sync(self._ctx))
+
+    def last_dispatch_ms(self) -> float:
+        ms = ctypes.c_float()
+        self._chk("pt_last_dispatch_ms", self._L.pt_last_dispatch_ms(self._ctx, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def read_image(self) -> np.ndarray:
+        """The accumulation image as float32 [height][width][4], row 0 = y 0."""
+        w, h = self.size
+        out = np.empty((h, w, 4), dtype=np.float32)
+        self._chk("pt_read_accum", self._L.pt_read_accum(self._ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                                          out.nbytes))
+        return out
+
+    # -- RCCL ------------------------------------------------------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * N.PT_COMM_ID_BYTES)()
+        N.check("pt_comm_get_unique_id", N.lib().pt_comm_get_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes) -> None:
+        buf = (ctypes.c_uint8 * N.PT_COMM_ID_BYTES).from_buffer_copy(uid)
+        self._chk("pt_comm_init", self._L.pt_comm_init(self._ctx, nranks, rank, buf))
+
+    def reduce(self, root: int = 0) -> None:
+        self._chk("pt_reduce_accum", self._L.pt_reduce_accum(self._ctx, root))
+
+    def read_reduced(self) -> np.ndarray:
+        w, h = self.size
+        out = np.empty((h, w, 4), dtype=np.float32)
+        self._chk("pt_read_reduced", self._L.pt_read_reduced(self._ctx, out.ctypes.data_as(
+            ctypes.POINTER(ctypes.c_float)), out.nbytes))
+        return out
+
+
+def save_image_rgba8(img: np.ndarray) -> np.ndarray:
+    """State::save_image pixel transform (state.rs:277-289): powf(1/2.2) * 255
+    as u8 (saturating, NaN -> 0), alpha * 255, rows flipped (row 0 = top)."""
+    v = img.astype(np.float32)
+    rgb = np.power(v[..., :3], np.float32(1.0 / 2.2)) * np.float32(255.0)
+    a = v[..., 3:4] * np.float32(255.0)
+    out = np.concatenate([rgb, a], axis=-1)
+    out = np.nan_to_num(out, nan=0.0, posinf=255.0, neginf=0.0)
+    out = np.clip(np.trunc(out), 0, 255).astype(np.uint8)
+    return out[::-1].copy()
+
+
+def save_png(img: np.ndarray, path: str) -> None:
+    from PIL import Image
+
+    Image.fromarray(save_image_rgba8(img), mode="RGBA").save(path)

@@ -1,0 +1,223 @@
+"""Synthetic scenes for BASELINE.json's configurations.
+
+All scenes are built through the editor mirror (:mod:`.sdf_editor`) so they
+exercise the same compile path a user scene takes.  Values are deterministic.
+
+* ``c1_default`` -- the editor's default scene (sdf_editor.rs:26-27: one Union
+  holding one unit Sphere, AABB on, exaggeration 1.3) with brightness 1 so the
+  image is not black (the default Material has brightness 0).
+* ``c2_sphere_box_torus`` -- (sphere U box) - torus expressed in the
+  reference's union semantics: header union A (Subtraction) = [torus, sphere]
+  -> sphere - torus; header union B (Subtraction) = [torus, box] -> box -
+  torus; the header level always unions, giving (sphere U box) - torus.  Plus
+  one emissive sphere.  The torus is a build extension (absent upstream).
+* ``c3_graph32`` -- a flat 32-node graph: 4 header unions x 7 shapes.  Union 0
+  is the Cornell-like room of the reference's saved scene assets/maps/test.json
+  (floor, roof, emissive light box, tilted back wall, two side walls; values
+  copied, light colour (0,0,0) of non-emitters replaced by the live editor's
+  default (1,1,1) because the current Mat normalises it), plus the two
+  rough-specular octahedra of that file in union 1; the rest is drawn from a
+  fixed PRNG (seed 42): spheres/cubes, sizes in [0.2, 0.75], rotations in
+  [-pi, pi]; unions 1-3 mix Union/Subtraction and carry their own transforms.
+  AABB culling is on for 24 of the 28 shapes.
+"""
+from __future__ import annotations
+
+import math
+from typing import Sequence
+
+import numpy as np
+
+from .sdf_editor import SDFEditor, Shape, Shapes, Union, UnionType
+
+
+def _mat(shape: Shape, col=(1, 1, 1), brightness=0.0, light=(1, 1, 1), spec=0.0, spec_col=(1, 1, 1), rough=0.0):
+    m = shape.material
+    m.color.set(col)
+    m.brightness.set(brightness)
+    m.light_col.set(light)
+    m.specular_chance.set(spec)
+    m.specular_color.set(spec_col)
+    m.roughness.set(rough)
+
+
+def _shape(kind: str, pos=(0, 0, 0), rot=(0, 0, 0), scale=1.0, size: Sequence[float] = (1.0,), aabb=True, name="Shape",
+           ex=1.3) -> Shape:
+    s = Shape(kind)
+    s.name = name
+    s.transform.position.set(pos)
+    s.transform.rotation.set(rot)
+    s.transform.scale.set(scale)
+    s.transform.aabb = aabb
+    s.transform.aabb_exaggeration.set(ex)
+    for p, v in zip(s.current_shape.params, size):
+        p.set(v)
+    return s
+
+
+def _union(name: str, union_type=UnionType.UNION, pos=(0, 0, 0), rot=(0, 0, 0), scale=1.0) -> Union:
+    u = Union(union_type)
+    u.name = name
+    u.transform.position.set(pos)
+    u.transform.rotation.set(rot)
+    u.transform.scale.set(scale)
+    return u
+
+
+def empty() -> SDFEditor:
+    """PLACEHOLDER_MAP (state.rs:20-36): no unions; every pixel misses."""
+    return SDFEditor([])
+
+
+def c1_default() -> SDFEditor:
+    ed = SDFEditor()  # Union + Sphere(1.0), defaults everywhere
+    _mat(ed.header_unions[0].children_shapes[0], brightness=1.0)
+    return ed
+
+
+def c2_sphere_box_torus() -> SDFEditor:
+    torus_rot = (1.2, 0.3, 0.0)
+
+    def torus():
+        t = _shape(Shapes.TORUS, pos=(0.0, 0.0, 0.2), rot=torus_rot, size=(1.05, 0.32), name="torus")
+        _mat(t, col=(0.15, 0.35, 0.95), spec=0.2, rough=0.4)
+        return t
+
+    a = _union("sphere-torus", UnionType.SUBTRACTION)
+    a.children_shapes.append(torus())
+    sph = _shape(Shapes.SPHERE, pos=(-0.75, 0.0, 0.3), size=(0.95,), name="sphere")
+    _mat(sph, col=(0.9, 0.25, 0.2))
+    a.children_shapes.append(sph)
+
+    b = _union("box-torus", UnionType.SUBTRACTION)
+    b.children_shapes.append(torus())
+    box = _shape(Shapes.CUBE, pos=(0.8, -0.1, 0.2), rot=(0.3, 0.6, 0.1), size=(0.7, 0.7, 0.7), name="box")
+    _mat(box, col=(0.85, 0.85, 0.8), spec=0.5, spec_col=(1.0, 0.9, 0.7), rough=0.25)
+    b.children_shapes.append(box)
+
+    light = _union("light")
+    ls = _shape(Shapes.SPHERE, pos=(0.0, 3.2, -0.5), size=(1.2,), name="light")
+    _mat(ls, col=(1, 1, 1), brightness=4.0)
+    light.children_shapes.append(ls)
+    floor = _shape(Shapes.CUBE, pos=(0.0, -2.0, 1.0), size=(6.0, 0.5, 6.0), name="floor")
+    _mat(floor, col=(0.6, 0.6, 0.6), spec=0.1, rough=0.6)
+    light.children_shapes.append(floor)
+    return SDFEditor([a, b, light])
+
+
+# assets/maps/test.json (deprecated node-editor save of the reference)
+_ROOM = [
+    ("floor", (11.63, 1.0, 12.26), (0.0, -2.32, 0.0), (0.0, 0.0, 0.0),
+     dict(col=(0.0, 0.6313726, 1.0), spec=0.75, spec_col=(0.50980395, 0.53333336, 1.0), rough=0.2)),
+    ("roof", (11.63, 1.0, 12.26), (0.0, 3.25, 0.0), (0.0, 0.0, 0.0),
+     dict(col=(0.0, 0.2509804, 1.0), spec=0.0, spec_col=(0.0, 0.0, 0.0), rough=0.0)),
+    ("light", (1.0, 1.0, 2.0), (0.0, 3.23, 1.85), (0.0, 0.0, 0.0),
+     dict(col=(0.0, 0.0, 0.0), brightness=1.2, light=(1.0, 1.0, 1.0), spec=0.0, spec_col=(0.0, 0.0, 0.0))),
+    ("4", (11.63, 1.0, 12.26), (0.0, 3.25, 3.75), (1.4, 0.0, 0.0),
+     dict(col=(1.0, 0.0, 0.0), spec=0.0, spec_col=(0.0, 0.0, 0.0))),
+    ("7", (1.0, 1.15, 7.2), (3.0, 0.0, 2.1), (0.0, -0.22, 0.0),
+     dict(col=(0.0, 0.0, 0.0), spec=0.5, spec_col=(1.0, 1.0, 1.0))),
+    ("8", (1.0, 1.15, 7.2), (-3.0, 0.0, 2.1), (0.0, 0.22, 0.0),
+     dict(col=(0.0, 0.0, 0.0), spec=0.5, spec_col=(1.0, 1.0, 1.0))),
+]
+_OCTA = [
+    ("5", 1.0, (0.0, -0.06, 1.8), (1.61, 2.82, 1.87)),
+    ("6", 1.0, (-0.05, -0.2, 1.8), (1.7, 1.8, 2.68)),
+]
+
+
+def c3_graph32(seed: int = 42) -> SDFEditor:
+    rng = np.random.default_rng(seed)
+    room = _union("room")
+    for name, size, pos, rot, mat in _ROOM:
+        s = _shape(Shapes.CUBE, pos=pos, rot=rot, size=size, name=name, aabb=name not in ("floor", "roof"))
+        _mat(s, **mat)
+        room.children_shapes.append(s)
+    # 7th room piece: a small emissive panel on the left wall
+    panel = _shape(Shapes.CUBE, pos=(-1.9, 1.2, 3.0), rot=(0.0, 0.22, 0.0), size=(0.05, 0.4, 0.8), name="panel")
+    _mat(panel, col=(1, 1, 1), brightness=2.5, light=(1.0, 0.85, 0.6))
+    room.children_shapes.append(panel)
+
+    specs = [
+        ("objects-a", UnionType.UNION, (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), 1.0),
+        ("objects-b", UnionType.SUBTRACTION, (0.6, 0.4, 0.8), (0.0, 0.5, 0.0), 0.9),
+        ("objects-c", UnionType.UNION, (-0.4, -0.3, 0.5), (0.2, -0.3, 0.1), 1.1),
+    ]
+    unions = [room]
+    for ui, (name, ut, upos, urot, usc) in enumerate(specs):
+        u = _union(name, ut, pos=upos, rot=urot, scale=usc)
+        first = 0
+        if ui == 0:
+            for oname, sz, opos, orot in _OCTA:
+                o = _shape(Shapes.OCTAHEDRON, pos=opos, rot=orot, size=(sz * 0.6,), name=oname)
+                _mat(o, col=(0.0, 0.0, 0.0), spec=1.0, spec_col=(1.0, 1.0, 1.0), rough=0.555)
+                u.children_shapes.append(o)
+            first = 2
+        for k in range(first, 7):
+            kind = Shapes.SPHERE if rng.random() < 0.5 else Shapes.CUBE
+            pos = (rng.uniform(-2.4, 2.4), rng.uniform(-1.2, 1.8), rng.uniform(-0.5, 4.0))
+            rot = tuple(rng.uniform(-math.pi, math.pi, 3))
+            if kind == Shapes.SPHERE:
+                size = (rng.uniform(0.2, 0.75),)
+            else:
+                size = tuple(rng.uniform(0.2, 0.75, 3))
+            # subtraction unions cut with their later members: keep those small
+            if ut == UnionType.SUBTRACTION and k > 0:
+                size = tuple(0.6 * v for v in size)
+            aabb = not (ui == 2 and k in (5, 6))
+            s = _shape(kind, pos=pos, rot=rot, size=size, aabb=aabb, name=f"{name}-{k}")
+            col = tuple(rng.uniform(0.1, 0.95, 3))
+            emissive = rng.random() < 0.12
+            spec = float(rng.choice([0.0, 0.0, 0.3, 0.8]))
+            _mat(s, col=col, brightness=3.0 if emissive else 0.0, spec=spec,
+                 spec_col=tuple(rng.uniform(0.6, 1.0, 3)), rough=float(rng.uniform(0.0, 0.6)))
+            u.children_shapes.append(s)
+        unions.append(u)
+    return SDFEditor(unions)
+
+
+def nested_demo() -> SDFEditor:
+    """Nested unions: exercises the compiler quirks of SURVEY.md A.9 (i)-(ii)
+    (child-union results discarded by the index-0 assignment; map/bounds
+    check[] index mismatch)."""
+    outer = _union("outer", UnionType.UNION, pos=(0.1, 0.0, 0.3), rot=(0.0, 0.3, 0.0), scale=0.9)
+    inner = _union("inner", UnionType.SUBTRACTION, pos=(0.3, 0.2, 0.0), scale=1.2)
+    a = _shape(Shapes.CUBE, pos=(0.0, 0.0, 0.0), size=(0.6, 0.6, 0.6), rot=(0.4, 0.1, 0.2))
+    _mat(a, col=(0.8, 0.3, 0.3))
+    b = _shape(Shapes.SPHERE, pos=(0.2, 0.2, -0.2), size=(0.5,))
+    _mat(b, col=(0.3, 0.8, 0.3))
+    inner.children_shapes += [a, b]
+    deeper = _union("deeper", UnionType.UNION, pos=(-0.5, 0.0, 0.0))
+    c = _shape(Shapes.OCTAHEDRON, pos=(0.0, 0.5, 0.0), size=(0.5,), rot=(0.3, 0.2, 0.1))
+    _mat(c, col=(0.3, 0.3, 0.9), spec=0.6, rough=0.2)
+    deeper.children_shapes.append(c)
+    inner.children_unions.append(deeper)
+    outer.children_unions.append(inner)
+    d = _shape(Shapes.SPHERE, pos=(-0.9, -0.2, 0.4), size=(0.45,))
+    _mat(d, col=(0.9, 0.9, 0.2), brightness=2.0)
+    e = _shape(Shapes.CUBE, pos=(0.9, -0.4, 0.0), size=(0.3, 0.5, 0.3), aabb=False)
+    _mat(e, col=(0.5, 0.5, 0.5), spec=0.4)
+    outer.children_shapes += [d, e]
+    top2 = _union("lamp")
+    l = _shape(Shapes.SPHERE, pos=(0.0, 2.5, 0.0), size=(0.8,))
+    _mat(l, brightness=3.0)
+    top2.children_shapes.append(l)
+    return SDFEditor([outer, top2])
+
+
+SCENES = {
+    "empty": empty,
+    "c1": c1_default,
+    "c2": c2_sphere_box_torus,
+    "c3": c3_graph32,
+    "nested": nested_demo,
+}
+
+# BASELINE.json configs -> (scene, width, height, spp, bounces)
+CONFIGS = {
+    "c1": ("c1", 256, 256, 1, 1),
+    "c2": ("c2", 1920, 1080, 64, 4),
+    "c3": ("c3", 1920, 1080, 256, 8),
+    "c4": ("c3", 3840, 2160, 256, 8),
+    "c5": ("c3", 1920, 1080, 1024, 16),
+}

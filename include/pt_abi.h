@@ -1,0 +1,186 @@
+/*
+ * pt_abi.h -- C ABI of the MI355X-native SDF path-trace hot path.
+ *
+ * This is the drop-in boundary that replaces the wgpu objects owned by the
+ * reference's `PathTracer` (src/path_tracer/path_tracer.rs:18-163), the
+ * `data[]` storage buffer of `DataArray` (src/sdf_editor/primitives.rs:59-157)
+ * and the GLSL text that `SDFEditor::compile` (src/sdf_editor/sdf_editor.rs:
+ * 186-246) splices into the compute shader.  Plain C types only; every entry
+ * point returns a status code (PT_OK = 0); `pt_last_error` explains failures.
+ * Inputs are borrowed and copied before return; outputs are caller-owned.
+ * Calls on one context are not re-entrant (the reference is single-threaded,
+ * src/inbuilt/event_loop.rs:7-76).  See INTEGRATION.md for the Rust binding.
+ */
+#ifndef PT_ABI_H
+#define PT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+/* status codes */
+#define PT_OK 0
+#define PT_ERR_INVALID -1      /* bad argument / malformed program or scene */
+#define PT_ERR_HIP -2          /* HIP runtime failure */
+#define PT_ERR_UNSUPPORTED -3  /* e.g. Shapes::Plane (containers.rs:287,295 emits NotImplemented) */
+#define PT_ERR_STATE -4        /* program/data missing, wrong call order */
+#define PT_ERR_RCCL -5         /* collective failure */
+#define PT_ERR_SIZE -6         /* caller buffer too small (required size written back) */
+
+typedef struct pt_ctx pt_ctx;
+
+/* == `Constants` UBO (path_tracer.rs:149-155, test_compute.glsl:6-11), 16 B */
+typedef struct {
+    float time;
+    int32_t frame;
+    float aspect;
+    int32_t last_clear;
+} pt_constants;
+
+/* == `Settings` UBO (path_tracer.rs:157-163, test_compute.glsl:13-19), 20 B */
+typedef struct {
+    int32_t debug;   /* 0 path trace, 1 normals, 2 albedo, 3 bounce heat map */
+    int32_t bounces;
+    float scale;
+    float fov;
+    int32_t aabb;    /* unused by the kernel, as upstream */
+} pt_settings;
+
+/* ---------------------------------------------------------------------
+ * Scene tree (the SDFEditor node graph, flattened) -> compiled program
+ * --------------------------------------------------------------------- */
+#define PT_NODE_UNION 0       /* containers.rs:8-15 */
+#define PT_NODE_SPHERE 1      /* containers.rs:260 */
+#define PT_NODE_CUBE 2        /* containers.rs:261 */
+#define PT_NODE_TORUS 3       /* extension: BASELINE.json config 2 (absent upstream) */
+#define PT_NODE_OCTAHEDRON 4  /* shapes.glsl:13-25 (deprecated editor format) */
+#define PT_NODE_PLANE 5       /* containers.rs:262, unimplemented upstream -> PT_ERR_UNSUPPORTED */
+
+#define PT_UNION_TYPE_UNION 0       /* containers.rs:244-252 */
+#define PT_UNION_TYPE_SUBTRACTION 1
+
+/* One Union or Shape.  A union's children are the later nodes whose `parent`
+ * is its index, in array order; parent -1 = SDFEditor.header_unions. */
+typedef struct {
+    int32_t kind;
+    int32_t parent;
+    int32_t union_type;
+    int32_t aabb;               /* Transform.aabb */
+    float scale;                /* Transform.scale */
+    float position[3];
+    float rotation[3];
+    float aabb_exaggeration;
+    float size[3];              /* sphere [0]; cube xyz; torus (R, r); octahedron [0] */
+    float material[18];         /* Material in Mat order (test_compute.glsl:45-59) */
+} pt_scene_node;
+
+#define PT_OP_UNION_BEGIN 0
+#define PT_OP_SHAPE 1
+#define PT_OP_UNION_END 2
+
+#define PT_COMBINE_ASSIGN 0       /* UnionType::compile index 0 (containers.rs:245-247) */
+#define PT_COMBINE_UNION 1        /* opUnion, shapes.glsl:72-74 */
+#define PT_COMBINE_SUBTRACTION 2  /* opSubtraction, shapes.glsl:76-81 */
+
+/* One statement of the generated `map()`; operands are data[] slot indices.
+ * Replaces the GLSL text of Union::compile / Shape::compile. */
+typedef struct {
+    uint32_t opcode;
+    uint32_t shape;          /* PT_NODE_* for SHAPE */
+    uint32_t combine;        /* how the result joins the enclosing accumulator */
+    int32_t check;           /* check[] index guarding a SHAPE, -1 = `if (true)` */
+    uint32_t scale;
+    uint32_t position[3];
+    uint32_t rotation[3];
+    uint32_t aabb_exaggeration;
+    uint32_t size[3];
+    uint32_t material[18];
+} pt_op;
+
+#define PT_SO_SCALAR 0  /* vec3(size[0])  sphere, octahedron */
+#define PT_SO_VEC3 1    /* size.xyz       cube */
+#define PT_SO_ONE 2     /* vec3(1.0)      (Plane; never reached) */
+#define PT_SO_TORUS 3   /* extension: vec3(R + r, r, R + r) */
+
+/* One `if (bool_hit(intersectAABB(...))) back[i] = true;` of the generated
+ * `bounds()` (Shape::aabb_compile, containers.rs:442-463). */
+typedef struct {
+    int32_t back;
+    uint32_t so_kind;
+    uint32_t union_position[3];
+    uint32_t union_scale;
+    uint32_t shape_position[3];
+    uint32_t shape_scale;
+    uint32_t size[3];
+    uint32_t aabb_exaggeration;
+} pt_aabb;
+
+/* Compile a scene tree exactly as SDFEditor::compile allocates data[] slots
+ * and check[] indices (sdf_editor.rs:186-246).  Two-call pattern: any output
+ * pointer may be NULL, sizes are always written; returns PT_ERR_SIZE if a
+ * capacity is too small.  Host-only, no GPU needed. */
+int pt_compile_scene(const pt_scene_node *nodes, uint32_t n_nodes,
+                     pt_op *ops, uint32_t ops_cap, uint32_t *n_ops,
+                     pt_aabb *aabbs, uint32_t aabb_cap, uint32_t *n_aabb,
+                     float *data, uint32_t data_cap, uint32_t *n_data,
+                     uint32_t *n_check);
+
+/* ---------------------------------------------------------------------
+ * Render context
+ * --------------------------------------------------------------------- */
+/* == StorageTexturePackage::new (structs.rs:113-160): RGBA32F image, zeroed.
+ * Device memory is row-major, row y = 0 first, 16 B per texel. */
+int pt_create(int hip_device, uint32_t width, uint32_t height, pt_ctx **out);
+/* == StorageTexturePackage::remake + `last_clear = 0` (path_tracer.rs:101-106) */
+int pt_resize_clear(pt_ctx *ctx, uint32_t width, uint32_t height);
+/* == PathTracer::remake_pipeline(map) (path_tracer.rs:62-76): topology change */
+int pt_set_program(pt_ctx *ctx, const pt_op *ops, uint32_t n_ops, const pt_aabb *aabbs, uint32_t n_aabb,
+                   uint32_t n_check);
+/* == DataArray::update (primitives.rs:131-151): value-only update, no recompile */
+int pt_set_data(pt_ctx *ctx, const float *data, uint32_t n);
+/* Multi-GPU tile ownership (new): 8x8 tile t is rendered iff t % nranks == rank.
+ * Clears the image (non-owned texels stay exactly 0). */
+int pt_set_tiles(pt_ctx *ctx, uint32_t rank, uint32_t nranks);
+/* == `spp` successive (PathTracer::update, compute_pass) pairs: frame j uses
+ * frame = c->frame + j and last_clear = c->last_clear + j (path_tracer.rs:
+ * 110-111).  Asynchronous, ordered on the context's HIP stream. */
+int pt_dispatch(pt_ctx *ctx, const pt_constants *c, const pt_settings *s, uint32_t spp);
+/* == State::save_image readback (state.rs:237-303): blocking copy of the
+ * local image (w*h*4 floats) into a caller buffer. */
+int pt_read_accum(pt_ctx *ctx, float *rgba, size_t bytes);
+/* Device pointer + size of the local image (for external collectives). */
+int pt_accum_device_ptr(pt_ctx *ctx, void **dev_ptr, size_t *bytes);
+int pt_get_size(const pt_ctx *ctx, uint32_t *width, uint32_t *height);
+
+/* RCCL over xGMI (new).  The 128-byte id is produced on one rank and
+ * broadcast by the caller's own channel (e.g. torch.distributed). */
+#define PT_COMM_ID_BYTES 128
+int pt_comm_get_unique_id(uint8_t id[PT_COMM_ID_BYTES]);
+int pt_comm_init(pt_ctx *ctx, uint32_t nranks, uint32_t rank, const uint8_t id[PT_COMM_ID_BYTES]);
+/* Sum of every rank's image into this context's result image on `root`
+ * (out of place: the local accumulation keeps progressing). */
+int pt_reduce_accum(pt_ctx *ctx, int root);
+int pt_read_reduced(pt_ctx *ctx, float *rgba, size_t bytes);
+
+int pt_sync(pt_ctx *ctx);
+/* Device time (HIP events on the context stream) of the kernels of the last
+ * pt_dispatch, in ms; blocks until they finished. */
+int pt_last_dispatch_ms(pt_ctx *ctx, float *ms);
+/* Instrumented re-run of one dispatch (does not touch the image): per-event
+ * work counters for algorithmic-flop accounting. */
+#define PT_STAT_COUNT 16
+int pt_dispatch_stats(pt_ctx *ctx, const pt_constants *c, const pt_settings *s, uint32_t spp,
+                      uint64_t counters[PT_STAT_COUNT]);
+const char *pt_last_error(const pt_ctx *ctx);
+void pt_destroy(pt_ctx *ctx);
+int pt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,16 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, short bench.  Stops at the first
+# step that crashes/times out (exit >= 2 other than a pytest failure code 1).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+timeout -k 10 600 python -m pytest tests -m gpu -q -s -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+ok $rc || exit $rc
+timeout -k 10 180 python __graft_entry__.py > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
+ok $rc || exit $rc
+timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
+exit $rc
