@@ -105,4 +105,11 @@ struct PtLaunch {
     float fov;
     float aspect;
     int32_t write;           // 0: instrumented run, leave the image untouched
+    int32_t kernel;          // PT_KERNEL_* (0 = choose)
+    int32_t shade_batch;     // wavefront kernel: shade when >= this many lanes wait
 };
+
+#define PT_KERNEL_AUTO 0
+#define PT_KERNEL_SIMPLE 1     // one path per lane, reference loop structure
+#define PT_KERNEL_WAVEFRONT 2  // per-lane state machine with job refill
+#define PT_RING 8              // wavefront kernel: in-flight samples per pixel

@@ -415,8 +415,352 @@ __global__ __launch_bounds__(64) void pt_render_kernel(PtLaunch L) {
 template __global__ void pt_render_kernel<false>(PtLaunch);
 template __global__ void pt_render_kernel<true>(PtLaunch);
 
+// ---------------------------------------------------------------------------
+// Wavefront kernel.  Same per-sample arithmetic as pt_render_kernel, different
+// schedule: each lane runs a state machine and every loop iteration performs
+// exactly one map() for every lane that is marching or taking a normal tap,
+// so march-length, bounce-count and Russian-roulette divergence no longer
+// idle lanes.  The tile's V pixels x spp frames form a job pool; a lane whose
+// path ends takes the next job (wave ballot + prefix count).  Finished samples
+// land in an LDS ring (PT_RING slots per pixel) and the pixel's owner lane
+// folds them in frame order, so the accumulation is bit-identical to the
+// reference's frame-by-frame mix (test_compute.glsl:242-245).  bounds() is
+// redistributed: the (ray, box) slab tests of all lanes that start a segment
+// are spread over the 64 lanes, one pair per lane per pass.
+// ---------------------------------------------------------------------------
+namespace {
+
+enum : int { ST_FREE = 0, ST_BOUNDS = 1, ST_MARCH = 2, ST_NORMAL = 3, ST_SHADE = 4 };
+
+struct WaveLds {
+    float col[PT_RING][3][64];
+    uint8_t ready[PT_RING][64];
+    int folded[64];
+    uint32_t mask[64][4];
+    int list[64];
+    int valid[64];
+};
+
+__device__ __forceinline__ int lane_rank(uint64_t m) {  // set bits of m below this lane
+    return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+}
+
+}  // namespace
+
+template <bool ST>
+__global__ __launch_bounds__(64) void pt_wave_kernel(PtLaunch L) {
+    __shared__ WaveLds S;
+    const int lane = int(threadIdx.x);
+    const int g = L.rank + int(blockIdx.x) * L.nranks;
+    const int tx0 = (g % L.tiles_x) * PT_TILE, ty0 = (g / L.tiles_x) * PT_TILE;
+    Stats<ST> st;
+    st.init();
+
+    // pixels of this tile inside the image, compacted (edge tiles are ragged)
+    const int my_x = tx0 + (lane & 7), my_y = ty0 + (lane >> 3);
+    const bool inside = my_x < L.width && my_y < L.height;
+    const uint64_t vmask = __ballot(inside);
+    const int V = __popcll(vmask);
+    const int vidx = lane_rank(vmask);
+    if (inside) S.valid[vidx] = lane;
+    S.folded[lane] = 0;
+#pragma unroll
+    for (int r = 0; r < PT_RING; ++r) S.ready[r][lane] = 0;
+
+    // debug 3 stores the last frame only; debug 0 folds every frame
+    const int j0 = L.debug != 0 ? L.spp - 1 : 0;
+    const int nsmp = L.spp - j0;
+    float ar = 0.0f, ag = 0.0f, ab = 0.0f;
+    float *texel = L.accum + (size_t(my_y) * size_t(L.width) + size_t(my_x)) * 4;
+    if (inside && L.debug == 0 && L.write) {
+        const float4 v = *reinterpret_cast<const float4 *>(texel);
+        ar = v.x;
+        ag = v.y;
+        ab = v.z;
+    }
+    int folded = 0;
+    __syncthreads();
+
+    // q / V for small q by multiply-high (exact for q < 2^16)
+    const uint32_t vmagic = V > 0 ? uint32_t((0x100000000ull + uint64_t(V) - 1) / uint64_t(V)) : 0u;
+    // bounds redistribution: (lane / n_aabb, lane % n_aabb) and the per-pass step
+    const int nbox = L.n_aabb;
+    const int la = nbox > 0 ? lane / nbox : 0, lb = nbox > 0 ? lane % nbox : 0;
+    const int da = nbox > 0 ? 64 / nbox : 0, db = nbox > 0 ? 64 % nbox : 0;
+    const PtAabb *__restrict__ boxes = L.aabbs;
+    const int shade_batch = L.shade_batch > 0 ? L.shade_batch : 1;
+
+    const int total = V * nsmp;
+    int next_p = 0, next_s = 0, issued = 0;  // wave-uniform issue cursor
+
+    // per-lane path state
+    int state = ST_FREE;
+    int jp = 0, js = 0;              // job: pixel slot, frame index
+    uint32_t rng = 0;
+    pt_f3 ro{0.0f, 0.0f, 0.0f}, rd{0.0f, 0.0f, 1.0f};
+    pt_f3 thr{1.0f, 1.0f, 1.0f}, ret{0.0f, 0.0f, 0.0f};
+    int seg = 0, step = 0, mat = 0;
+    float t = 0.0f;
+    float dv0 = 0.0f, dv1 = 0.0f, dv2 = 0.0f;
+    Check ck{0ull, 0ull};
+
+    for (;;) {
+        // ---- 1. refill free lanes from the job pool (in job order) -------
+        const uint64_t freem = __ballot(state == ST_FREE);
+        if (freem != 0ull && issued < total) {
+            const int r = lane_rank(freem);
+            const uint32_t q = uint32_t(next_p + r);
+            const int wrap = int(__umulhi(q, vmagic));
+            const int p = int(q) - wrap * V;
+            const int s = next_s + wrap;
+            const bool cand = state == ST_FREE && issued + r < total;
+            const bool ok = cand && s < S.folded[p] + PT_RING;
+            const uint64_t candm = __ballot(cand), bad = candm & ~__ballot(ok);
+            int n = __popcll(candm);
+            if (bad != 0ull) {
+                const int first_bad = __builtin_ctzll(bad);
+                n = __popcll(freem & ((1ull << first_bad) - 1ull));
+            }
+            if (cand && r < n) {
+                jp = p;
+                js = s;
+                const int lp = S.valid[p];
+                const int x = tx0 + (lp & 7), y = ty0 + (lp >> 3);
+                const int32_t frame = int32_t(uint32_t(L.frame0) + uint32_t(j0 + s));
+                rng = pt_gen_rng(x, y, frame, L.width, L.height);
+                float jx = pt_random01(rng);
+                float jy = pt_random01(rng);
+                jx = jx - 0.5f;
+                jy = jy - 0.5f;
+                float ux = (float(x) + jx) / float(L.width), uy = (float(y) + jy) / float(L.height);
+                ux = ux * 2.0f - 1.0f;
+                uy = uy * 2.0f - 1.0f;
+                ux *= L.aspect;
+                rd = pt_normalize(pt_f3{ux, uy, L.fov});
+                ro = pt_f3{0.0f, 0.0f, -3.0f};
+                thr = pt_f3{1.0f, 1.0f, 1.0f};
+                ret = pt_f3{0.0f, 0.0f, 0.0f};
+                seg = 0;
+                state = ST_BOUNDS;
+                st.add(PT_ST_SAMPLES);
+            }
+            // advance the cursor by n jobs
+            const uint32_t qn = uint32_t(next_p + n);
+            const int wn = int(__umulhi(qn, vmagic));
+            next_p = int(qn) - wn * V;
+            next_s += wn;
+            issued += n;
+        }
+
+        // ---- 2. bounds() for lanes starting a segment, (ray, box) pairs ---
+        const uint64_t needm = __ballot(state == ST_BOUNDS);
+        if (needm != 0ull) {
+            if (state == ST_BOUNDS) {
+                S.list[lane_rank(needm)] = lane;
+                S.mask[lane][0] = S.mask[lane][1] = S.mask[lane][2] = S.mask[lane][3] = 0u;
+                st.add(PT_ST_SEGMENTS);
+            }
+            __syncthreads();
+            const int pairs = __popcll(needm) * nbox;
+            int a = la, b = lb;
+            for (int base = 0; base < pairs; base += 64) {
+                const bool act = base + lane < pairs;
+                const int src = act ? S.list[a] : lane;
+                const float ox = __shfl(ro.x, src, 64), oy = __shfl(ro.y, src, 64), oz = __shfl(ro.z, src, 64);
+                const float dx = __shfl(rd.x, src, 64), dy = __shfl(rd.y, src, 64), dz = __shfl(rd.z, src, 64);
+                if (act) {
+                    const PtAabb bx = boxes[b];
+                    const float tminx = (bx.bmin[0] - ox) / dx, tmaxx = (bx.bmax[0] - ox) / dx;
+                    const float tminy = (bx.bmin[1] - oy) / dy, tmaxy = (bx.bmax[1] - oy) / dy;
+                    const float tminz = (bx.bmin[2] - oz) / dz, tmaxz = (bx.bmax[2] - oz) / dz;
+                    const float tnear = pt_gmax(pt_gmax(pt_gmin(tminx, tmaxx), pt_gmin(tminy, tmaxy)), pt_gmin(tminz, tmaxz));
+                    const float tfar = pt_gmin(pt_gmin(pt_gmax(tminx, tmaxx), pt_gmax(tminy, tmaxy)), pt_gmax(tminz, tmaxz));
+                    st.add(PT_ST_AABB);
+                    if (tnear < tfar && tfar > 0.0f) atomicOr(&S.mask[src][bx.back >> 5], 1u << (bx.back & 31));
+                }
+                a += da;
+                b += db;
+                if (b >= nbox) {
+                    b -= nbox;
+                    a += 1;
+                }
+            }
+            __syncthreads();
+            if (state == ST_BOUNDS) {
+                ck.lo = uint64_t(S.mask[lane][0]) | (uint64_t(S.mask[lane][1]) << 32);
+                ck.hi = uint64_t(S.mask[lane][2]) | (uint64_t(S.mask[lane][3]) << 32);
+                t = 0.0f;
+                step = 0;
+                state = ST_MARCH;
+            }
+        }
+
+        // ---- 3. one map() per marching / normal-tap lane ---------------------
+        const bool mapping = state == ST_MARCH || state == ST_NORMAL;
+        if (__ballot(mapping) != 0ull) {
+            if (mapping) {
+                float qx, qy, qz;
+                if (state == ST_MARCH) {  // CastRay: p = ro + rd * t
+                    qx = ro.x + rd.x * t;
+                    qy = ro.y + rd.y * t;
+                    qz = ro.z + rd.z * t;
+                } else {  // calc_normal tap `step` around hit point (held in ro)
+                    const float e = 0.0001f;
+                    const int axis = step >> 1;
+                    const bool neg = (step & 1) != 0;
+                    const float on = neg ? -e : e, off = neg ? -0.0f : 0.0f;
+                    qx = ro.x + (axis == 0 ? on : off);
+                    qy = ro.y + (axis == 1 ? on : off);
+                    qz = ro.z + (axis == 2 ? on : off);
+                }
+                const Hit h = scene_map<ST>(L, qx, qy, qz, ck, st);
+                // ---- 4. advance the state machine ------------------------------
+                if (state == ST_MARCH) {
+                    st.add(PT_ST_MARCH);
+                    mat = h.m;
+                    t += h.d;
+                    ++step;
+                    if (fabsf(h.d) < kMhd || t > kFp || step == kSteps) {
+                        if (t > kFp) {
+                            state = ST_SHADE;  // miss: path ends (seg stays)
+                            step = -1;
+                        } else {
+                            ro = pt_f3{ro.x + rd.x * t, ro.y + rd.y * t, ro.z + rd.z * t};  // calc_point
+                            state = ST_NORMAL;
+                            step = 0;
+                        }
+                    }
+                } else {
+                    if ((step & 1) == 0) {
+                        t = h.d;  // d(p + e)
+                    } else {
+                        const float dd = t - h.d;
+                        if (step == 1) dv0 = dd;
+                        else if (step == 3) dv1 = dd;
+                        else dv2 = dd;
+                    }
+                    ++step;
+                    if (step == 6) {
+                        st.add(PT_ST_NORMAL_MAPS, 6);
+                        state = ST_SHADE;
+                    }
+                }
+            }
+        }
+
+        // ---- 5. shading (batched) and path completion ----------------------
+        const uint64_t shadem = __ballot(state == ST_SHADE);
+        if (shadem != 0ull &&
+            (__popcll(shadem) >= shade_batch || __ballot(state == ST_MARCH || state == ST_NORMAL) == 0ull ||
+             issued >= total)) {
+            if (state == ST_SHADE) {
+                bool done = step < 0;  // miss
+                if (!done) {
+                    const pt_f3 n = pt_normalize(pt_f3{dv0, dv1, dv2});
+                    const pt_f3 hp = ro;
+                    ro = pt_f3{hp.x + n.x * kOffset, hp.y + n.y * kOffset, hp.z + n.z * kOffset};
+                    st.add(PT_ST_SHADED);
+                    const PtMat &m = L.mats[mat];
+                    const float spec_chance = m.spec;
+                    const bool do_spec = pt_random01(rng) < spec_chance;
+                    float ray_prob = do_spec ? spec_chance : 1.0f - spec_chance;
+                    ray_prob = pt_gmax(ray_prob, 0.0001f);
+                    const float uz = pt_random01(rng) * 2.0f - 1.0f;
+                    const float ua = pt_random01(rng) * kPi2;
+                    const float ur = sqrtf(1.0f - uz * uz);
+                    float sa, ca;
+                    pt_sincos(ua, sa, ca);
+                    const pt_f3 diffuse = pt_normalize(pt_f3{n.x + ur * ca, n.y + ur * sa, n.z + uz});
+                    if (do_spec) {
+                        const float k = 2.0f * pt_dot(n, rd);
+                        const pt_f3 sr{rd.x - k * n.x, rd.y - k * n.y, rd.z - k * n.z};
+                        const float al = m.rough2, oma = 1.0f - al;
+                        rd = pt_normalize(pt_f3{sr.x * oma + diffuse.x * al, sr.y * oma + diffuse.y * al,
+                                                sr.z * oma + diffuse.z * al});
+                    } else {
+                        rd = diffuse;
+                    }
+                    const float fs = do_spec ? 1.0f : 0.0f, omf = 1.0f - fs;
+                    ret.x += m.emis[0] * thr.x;
+                    ret.y += m.emis[1] * thr.y;
+                    ret.z += m.emis[2] * thr.z;
+                    thr.x *= m.col[0] * omf + m.spec_col[0] * fs;
+                    thr.y *= m.col[1] * omf + m.spec_col[1] * fs;
+                    thr.z *= m.col[2] * omf + m.spec_col[2] * fs;
+                    thr.x /= ray_prob;
+                    thr.y /= ray_prob;
+                    thr.z /= ray_prob;
+                    const float pmax = pt_gmax(thr.x, pt_gmax(thr.y, thr.z));
+                    if (pt_random01(rng) > pmax) {
+                        st.add(PT_ST_RR_BREAK);
+                        done = true;
+                    } else {
+                        const float ip = 1.0f / pmax;
+                        thr.x *= ip;
+                        thr.y *= ip;
+                        thr.z *= ip;
+                        ++seg;
+                        if (seg > L.bounces) done = true;
+                        else state = ST_BOUNDS;
+                    }
+                }
+                if (done) {
+                    pt_f3 c = ret;
+                    if (L.debug == 3) {
+                        const float v = float(seg) / float(L.bounces);
+                        c = pt_f3{v, v, v};
+                    }
+                    const int slot = js & (PT_RING - 1);
+                    S.col[slot][0][jp] = c.x;
+                    S.col[slot][1][jp] = c.y;
+                    S.col[slot][2][jp] = c.z;
+                    S.ready[slot][jp] = 1;
+                    state = ST_FREE;
+                }
+            }
+            __syncthreads();
+            // ---- 6. owners fold finished frames in order --------------------
+            if (inside) {
+                for (;;) {
+                    const int slot = folded & (PT_RING - 1);
+                    if (folded >= nsmp || S.ready[slot][vidx] == 0) break;
+                    const float cr = S.col[slot][0][vidx], cg = S.col[slot][1][vidx], cb = S.col[slot][2][vidx];
+                    if (L.debug != 0) {
+                        ar = cr;
+                        ag = cg;
+                        ab = cb;
+                    } else {
+                        const int32_t lc = int32_t(uint32_t(L.last_clear0) + uint32_t(j0 + folded));
+                        const float w = 1.0f / float(lc + 1), omw = 1.0f - w;
+                        ar = ar * omw + cr * w;
+                        ag = ag * omw + cg * w;
+                        ab = ab * omw + cb * w;
+                    }
+                    S.ready[slot][vidx] = 0;
+                    ++folded;
+                }
+                S.folded[vidx] = folded;
+            }
+            __syncthreads();
+        }
+
+        if (issued >= total && __ballot(state != ST_FREE) == 0ull) break;
+    }
+    if (inside && L.write) *reinterpret_cast<float4 *>(texel) = make_float4(ar, ag, ab, 1.0f);
+    flush_stats<ST>(L, st);
+}
+
+template __global__ void pt_wave_kernel<false>(PtLaunch);
+template __global__ void pt_wave_kernel<true>(PtLaunch);
+
 void pt_launch_render(const PtLaunch &L, bool stats, hipStream_t stream) {
     dim3 grid(unsigned(L.n_tiles)), block(64);
-    if (stats) hipLaunchKernelGGL(pt_render_kernel<true>, grid, block, 0, stream, L);
-    else hipLaunchKernelGGL(pt_render_kernel<false>, grid, block, 0, stream, L);
+    const bool simple = L.kernel == PT_KERNEL_SIMPLE || L.debug == 1 || L.debug == 2;
+    if (simple) {
+        if (stats) hipLaunchKernelGGL(pt_render_kernel<true>, grid, block, 0, stream, L);
+        else hipLaunchKernelGGL(pt_render_kernel<false>, grid, block, 0, stream, L);
+    } else {
+        if (stats) hipLaunchKernelGGL(pt_wave_kernel<true>, grid, block, 0, stream, L);
+        else hipLaunchKernelGGL(pt_wave_kernel<false>, grid, block, 0, stream, L);
+    }
 }

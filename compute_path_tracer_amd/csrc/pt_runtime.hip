@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -52,6 +53,9 @@ struct pt_ctx {
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    // options (pt_set_option)
+    int kernel = -1;       // PT_KERNEL_*; -1 = environment / auto
+    int shade_batch = -1;  // -1 = environment / default
     std::string err;
 };
 
@@ -341,6 +345,20 @@ static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, u
     L.fov = s->fov;
     L.aspect = k->aspect;
     L.write = 1;
+    // tuning knobs (A/B experiments; defaults are the shipped configuration)
+    static const int env_kernel = [] {
+        const char *v = std::getenv("PT_KERNEL");
+        if (!v) return PT_KERNEL_AUTO;
+        if (!std::strcmp(v, "simple")) return PT_KERNEL_SIMPLE;
+        if (!std::strcmp(v, "wave")) return PT_KERNEL_WAVEFRONT;
+        return PT_KERNEL_AUTO;
+    }();
+    static const int env_batch = [] {
+        const char *v = std::getenv("PT_SHADE_BATCH");
+        return v ? std::atoi(v) : 0;
+    }();
+    L.kernel = c->kernel >= 0 ? c->kernel : env_kernel;
+    L.shade_batch = c->shade_batch > 0 ? c->shade_batch : (env_batch > 0 ? env_batch : 1);
     return PT_OK;
 }
 
@@ -475,6 +493,21 @@ int pt_last_dispatch_ms(pt_ctx *c, float *ms) {
     HIPCHK(c, hipEventSynchronize(c->ev1));
     HIPCHK(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
     return PT_OK;
+}
+
+int pt_set_option(pt_ctx *c, const char *key, int value) {
+    if (!c || !key) return PT_ERR_INVALID;
+    if (!std::strcmp(key, "kernel")) {
+        if (value < PT_KERNEL_AUTO || value > PT_KERNEL_WAVEFRONT) return fail(c, PT_ERR_INVALID, "bad kernel id");
+        c->kernel = value;
+        return PT_OK;
+    }
+    if (!std::strcmp(key, "shade_batch")) {
+        if (value < 1 || value > 64) return fail(c, PT_ERR_INVALID, "shade_batch must be in [1, 64]");
+        c->shade_batch = value;
+        return PT_OK;
+    }
+    return fail(c, PT_ERR_INVALID, std::string("unknown option ") + key);
 }
 
 const char *pt_last_error(const pt_ctx *c) { return c ? c->err.c_str() : "null context"; }

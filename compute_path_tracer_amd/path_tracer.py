@@ -124,6 +124,13 @@ class PathTracer:
                                                                   ctypes.byref(self.settings), spp, buf))
         return dict(zip(N.STAT_NAMES, (int(v) for v in buf)))
 
+    KERNELS = {"auto": 0, "simple": 1, "wave": 2}
+
+    def set_option(self, key: str, value) -> None:
+        if key == "kernel" and isinstance(value, str):
+            value = self.KERNELS[value]
+        self._chk("pt_set_option", self._L.pt_set_option(self._ctx, key.encode(), int(value)))
+
     def set_tiles(self, rank: int, nranks: int) -> None:
         self._chk("pt_set_tiles", self._L.pt_set_tiles(self._ctx, rank, nranks))
 

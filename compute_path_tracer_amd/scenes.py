@@ -193,13 +193,15 @@ def nested_demo() -> SDFEditor:
     deeper.children_shapes.append(c)
     inner.children_unions.append(deeper)
     outer.children_unions.append(inner)
-    d = _shape(Shapes.SPHERE, pos=(-0.9, -0.2, 0.4), size=(0.45,))
+    # emitters with aabb off: under quirk (ii) an aabb-guarded shape of a nested
+    # graph reads a check[] entry bounds() never sets, and would stay dark
+    d = _shape(Shapes.SPHERE, pos=(-0.9, -0.2, 0.4), size=(0.45,), aabb=False)
     _mat(d, col=(0.9, 0.9, 0.2), brightness=2.0)
     e = _shape(Shapes.CUBE, pos=(0.9, -0.4, 0.0), size=(0.3, 0.5, 0.3), aabb=False)
     _mat(e, col=(0.5, 0.5, 0.5), spec=0.4)
     outer.children_shapes += [d, e]
     top2 = _union("lamp")
-    l = _shape(Shapes.SPHERE, pos=(0.0, 2.5, 0.0), size=(0.8,))
+    l = _shape(Shapes.SPHERE, pos=(0.0, 2.5, 0.0), size=(0.8,), aabb=False)
     _mat(l, brightness=3.0)
     top2.children_shapes.append(l)
     return SDFEditor([outer, top2])

@@ -176,6 +176,10 @@ int pt_last_dispatch_ms(pt_ctx *ctx, float *ms);
 #define PT_STAT_COUNT 16
 int pt_dispatch_stats(pt_ctx *ctx, const pt_constants *c, const pt_settings *s, uint32_t spp,
                       uint64_t counters[PT_STAT_COUNT]);
+/* Tuning knobs: "kernel" (0 auto, 1 simple one-path-per-lane, 2 wavefront
+ * state machine) and "shade_batch" (wavefront kernel: lanes that must wait
+ * before a shading pass runs, 1..64).  Results are identical for every value. */
+int pt_set_option(pt_ctx *ctx, const char *key, int value);
 const char *pt_last_error(const pt_ctx *ctx);
 void pt_destroy(pt_ctx *ctx);
 int pt_abi_version(void);

@@ -19,10 +19,14 @@ pytestmark = pytest.mark.gpu
 RMS_TOL = 1e-5
 
 
-def _render_pair(ed, w, h, spp, bounces, debug=0, frame=1, last_clear=1, fov=1.0, aspect=None):
+def _render_pair(ed, w, h, spp, bounces, debug=0, frame=1, last_clear=1, fov=1.0, aspect=None, kernel="auto",
+                 shade_batch=None):
     prog = ed.compile(CompData())
     st = N.Settings(debug=debug, bounces=bounces, scale=1.0, fov=fov, aabb=0)
     pt = PathTracer(w, h, prog, settings=st)
+    pt.set_option("kernel", kernel)
+    if shade_batch:
+        pt.set_option("shade_batch", shade_batch)
     a = float(np.float32(w) / np.float32(h)) if aspect is None else aspect
     pt.dispatch(N.Constants(time=0.0, frame=frame, aspect=a, last_clear=last_clear), spp)
     gpu = pt.read_image()
@@ -41,26 +45,44 @@ def _report(gpu, ref):
     return rms, exact
 
 
+@pytest.mark.parametrize("kernel", ["simple", "wave"])
 @pytest.mark.parametrize("name,w,h,spp,bounces", [
     ("c1", 256, 256, 1, 1),        # BASELINE config 1 in full
     ("c2", 96, 64, 4, 4),
     ("c3", 96, 54, 2, 8),
     ("nested", 64, 64, 3, 6),
 ])
-def test_parity_path_trace(gpu, name, w, h, spp, bounces):
-    gpu_img, ref = _render_pair(scenes.SCENES[name](), w, h, spp, bounces)
+def test_parity_path_trace(gpu, name, w, h, spp, bounces, kernel):
+    gpu_img, ref = _render_pair(scenes.SCENES[name](), w, h, spp, bounces, kernel=kernel)
     rms, exact = _report(gpu_img, ref)
-    print(f"{name}: rms={rms:.3e} bit-exact={exact:.5f} mean={ref[..., :3].mean():.5f}")
+    print(f"{kernel} {name}: rms={rms:.3e} bit-exact={exact:.5f} mean={ref[..., :3].mean():.5f}")
     assert ref[..., :3].mean() > 0
     assert rms < RMS_TOL
     assert exact == 1.0
 
 
+@pytest.mark.parametrize("kernel", ["simple", "wave"])
 @pytest.mark.parametrize("debug", [1, 2, 3])
-def test_parity_debug_views(gpu, debug):
-    gpu_img, ref = _render_pair(scenes.c3_graph32(), 80, 45, 2, 8, debug=debug)
+def test_parity_debug_views(gpu, debug, kernel):
+    gpu_img, ref = _render_pair(scenes.c3_graph32(), 80, 45, 2, 8, debug=debug, kernel=kernel)
     rms, exact = _report(gpu_img, ref)
     assert rms < RMS_TOL and exact == 1.0
+
+
+@pytest.mark.parametrize("shade_batch", [1, 7, 64])
+def test_wave_kernel_schedule_invariance(gpu, shade_batch):
+    """Shading batch size changes the schedule only, never the result; spp
+    above the LDS ring size exercises the in-order fold."""
+    gpu_img, ref = _render_pair(scenes.c3_graph32(), 40, 24, 19, 8, kernel="wave", shade_batch=shade_batch)
+    rms, exact = _report(gpu_img, ref)
+    assert exact == 1.0, (shade_batch, rms)
+
+
+def test_long_dispatch_chunks(gpu):
+    """spp > 64 is split into several launches that continue frame/last_clear."""
+    gpu_img, ref = _render_pair(scenes.c1_default(), 16, 16, 70, 1)
+    rms, exact = _report(gpu_img, ref)
+    assert exact == 1.0
 
 
 def test_empty_scene_is_black(gpu):
