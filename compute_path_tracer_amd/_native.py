@@ -37,7 +37,8 @@ SYMBOLS = (
     "pt_compile_scene", "pt_create", "pt_resize_clear", "pt_set_program", "pt_set_data", "pt_set_tiles",
     "pt_dispatch", "pt_read_accum", "pt_accum_device_ptr", "pt_get_size", "pt_comm_get_unique_id",
     "pt_comm_init", "pt_reduce_accum", "pt_read_reduced", "pt_sync", "pt_last_dispatch_ms",
-    "pt_dispatch_stats", "pt_set_option", "pt_last_error", "pt_destroy", "pt_abi_version",
+    "pt_dispatch_stats", "pt_set_option", "pt_get_option", "pt_jit_log", "pt_jit_compile", "pt_last_error",
+    "pt_destroy", "pt_abi_version",
 )
 
 
@@ -120,6 +121,10 @@ def lib() -> ctypes.CDLL:
         "pt_last_dispatch_ms": (c_int, [ctx, POINTER(c_float)]),
         "pt_dispatch_stats": (c_int, [ctx, POINTER(Constants), POINTER(Settings), c_uint32, POINTER(c_uint64)]),
         "pt_set_option": (c_int, [ctx, c_char_p, c_int]),
+        "pt_get_option": (c_int, [ctx, c_char_p, POINTER(ctypes.c_double)]),
+        "pt_jit_log": (c_char_p, [ctx]),
+        "pt_jit_compile": (c_int, [POINTER(Op), c_uint32, POINTER(Aabb), c_uint32, POINTER(c_float), c_uint32, c_char_p,
+                                   c_size_t, POINTER(c_size_t)]),
         "pt_last_error": (c_char_p, [ctx]),
         "pt_destroy": (None, [ctx]),
         "pt_abi_version": (c_int, []),

@@ -13,9 +13,12 @@
 // same rounding (IEEE f32, no contraction) as the kernel would.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <cstdint>
+#endif
 
-#include "../../include/pt_abi.h"
+#include "pt_math.h"  // (hipRTC: provides the fixed-width typedefs)
+#include "pt_abi.h"
 
 #define PT_MAX_DEPTH 8      // union nesting supported by the interpreter
 #define PT_MAX_CHECK 128    // check[] entries (two 64-bit lane masks)

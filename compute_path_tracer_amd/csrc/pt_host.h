@@ -1,0 +1,31 @@
+// pt_host.h -- host-side internals shared by pt_runtime.hip and pt_jit.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "pt_device.h"
+
+// Expand (program, data[]) into the device tables (see pt_device.h).
+int pt_derive(const std::vector<pt_op> &ops, const std::vector<pt_aabb> &aabbs, const float *data, uint32_t n,
+              std::vector<PtNode> &nodes, std::vector<PtAabb> &boxes, std::vector<PtMat> &mats, std::string &err);
+
+// Scene-specialised kernels (hipRTC).
+struct PtJitModule {
+    hipModule_t module = nullptr;
+    hipFunction_t render = nullptr;
+    hipFunction_t render_stats = nullptr;
+    std::string key;  // generated source
+};
+
+// Source of the specialised kernel for these derived nodes (only the
+// topology, per-node flags and material indices enter; values stay in the
+// node table so value-only edits do not recompile).
+std::string pt_jit_source(const std::vector<PtNode> &nodes);
+// Compile with hipRTC for gfx950; returns the code object or an error log.
+bool pt_jit_compile_source(const std::string &src, std::vector<char> &code, std::string &log);
+// Load a code object on the current device.
+bool pt_jit_load(const std::vector<char> &code, PtJitModule &m, std::string &err);
+void pt_jit_unload(PtJitModule &m);

@@ -7,10 +7,18 @@
 // contract of DESIGN.md section 3 that makes host and device agree bitwise.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdint>
+#else  // hipRTC (per-scene JIT, pt_jit.cpp): no std headers
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::uint64_t uint64_t;
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::size_t size_t;
+#endif
 
 #define PT_HD __host__ __device__ __forceinline__
 

@@ -8,6 +8,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <map>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -17,9 +20,11 @@
 
 #include "../../include/pt_abi.h"
 #include "pt_device.h"
+#include "pt_host.h"
 #include "pt_math.h"
 
 void pt_launch_render(const PtLaunch &L, bool stats, hipStream_t stream);
+bool pt_use_simple_kernel(const PtLaunch &L);
 
 static_assert(sizeof(pt_constants) == 16, "Constants is 16 B (path_tracer.rs:149-155)");
 static_assert(sizeof(pt_settings) == 20, "Settings is 20 B (path_tracer.rs:157-163)");
@@ -56,10 +61,70 @@ struct pt_ctx {
     // options (pt_set_option)
     int kernel = -1;       // PT_KERNEL_*; -1 = environment / auto
     int shade_batch = -1;  // -1 = environment / default
+    int jit = -1;          // 1 use per-scene hipRTC kernels, 0 interpreter; -1 = env (PT_JIT), default 1
+    PtJitModule jit_mod;   // loaded scene kernel (key = its source)
+    std::string jit_log;
+    double jit_seconds = 0.0;
     std::string err;
 };
 
 namespace {
+
+// code objects by generated source, shared by every context of the process
+std::map<std::string, std::vector<char>> &jit_cache() {
+    static std::map<std::string, std::vector<char>> cache;
+    return cache;
+}
+std::mutex &jit_mutex() {
+    static std::mutex m;
+    return m;
+}
+
+bool jit_wanted(const pt_ctx *c) {
+    if (c->jit >= 0) return c->jit != 0;
+    static const int env = [] {
+        const char *v = std::getenv("PT_JIT");
+        return v ? std::atoi(v) : 1;
+    }();
+    return env != 0;
+}
+
+// (Re)build the scene-specialised kernel when the generated source changed.
+// A failure leaves the interpreter kernel in use and records the log.
+void jit_refresh(pt_ctx *c, const std::vector<PtNode> &nodes) {
+    if (!jit_wanted(c)) {
+        pt_jit_unload(c->jit_mod);
+        return;
+    }
+    std::string src = pt_jit_source(nodes);
+    if (c->jit_mod.module && c->jit_mod.key == src) return;
+    pt_jit_unload(c->jit_mod);
+    std::vector<char> code;
+    {
+        std::lock_guard<std::mutex> g(jit_mutex());
+        auto it = jit_cache().find(src);
+        if (it != jit_cache().end()) {
+            code = it->second;
+        } else {
+            const auto t0 = std::chrono::steady_clock::now();
+            std::string log;
+            const bool ok = pt_jit_compile_source(src, code, log);
+            c->jit_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (!ok) {
+                c->jit_log = "hipRTC compile failed: " + log;
+                return;
+            }
+            jit_cache()[src] = code;
+        }
+    }
+    std::string err;
+    if (!pt_jit_load(code, c->jit_mod, err)) {
+        c->jit_log = err;
+        return;
+    }
+    c->jit_mod.key = std::move(src);
+    c->jit_log.clear();
+}
 
 int fail(pt_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
@@ -98,10 +163,16 @@ int alloc_image(pt_ctx *c, uint32_t w, uint32_t h) {
 // Host expansion of (program, data[]) into the device tables.  Every value is
 // the f32 expression the generated GLSL evaluates on the GPU, evaluated here
 // once with the same rounding (see pt_device.h).
-int derive(pt_ctx *c, const float *data, uint32_t n, std::vector<PtNode> &nodes, std::vector<PtAabb> &boxes,
-           std::vector<PtMat> &mats) {
+}  // namespace
+
+int pt_derive(const std::vector<pt_op> &ops, const std::vector<pt_aabb> &aabbs, const float *data, uint32_t n,
+              std::vector<PtNode> &nodes, std::vector<PtAabb> &boxes, std::vector<PtMat> &mats, std::string &err) {
+    auto bad = [&](const char *msg) {
+        err = msg;
+        return PT_ERR_INVALID;
+    };
     auto in = [&](uint32_t s) { return s < n; };
-    nodes.resize(c->ops.size());
+    nodes.resize(ops.size());
     mats.clear();
     PtMat mdef;
     std::memset(&mdef, 0, sizeof mdef);
@@ -113,18 +184,18 @@ int derive(pt_ctx *c, const float *data, uint32_t n, std::vector<PtNode> &nodes,
         mdef.emis[2] = nl.z * 0.0f;
     }
     mats.push_back(mdef);
-    for (size_t i = 0; i < c->ops.size(); ++i) {
-        const pt_op &op = c->ops[i];
+    for (size_t i = 0; i < ops.size(); ++i) {
+        const pt_op &op = ops[i];
         PtNode &d = nodes[i];
         std::memset(&d, 0, sizeof d);
         d.op = int32_t(op.opcode);
         d.shape = int32_t(op.shape);
         d.combine = int32_t(op.combine);
         d.check = op.check;
-        if (!in(op.scale)) return fail(c, PT_ERR_INVALID, "op references data slot out of range");
+        if (!in(op.scale)) return bad("op references data slot out of range");
         for (int k = 0; k < 3; ++k)
             if (!in(op.position[k]) || !in(op.rotation[k]))
-                return fail(c, PT_ERR_INVALID, "op references data slot out of range");
+                return bad("op references data slot out of range");
         const float s = data[op.scale];
         const float inv = 1.0f / s;  // `1.0 / data[scale]`
         d.inv = inv;
@@ -141,11 +212,11 @@ int derive(pt_ctx *c, const float *data, uint32_t n, std::vector<PtNode> &nodes,
         d.flags = f;
         if (op.opcode == PT_OP_SHAPE) {
             for (int k = 0; k < 3; ++k) {
-                if (!in(op.size[k])) return fail(c, PT_ERR_INVALID, "size slot out of range");
+                if (!in(op.size[k])) return bad("size slot out of range");
                 d.size[k] = data[op.size[k]];
             }
             for (int k = 0; k < 18; ++k)
-                if (!in(op.material[k])) return fail(c, PT_ERR_INVALID, "material slot out of range");
+                if (!in(op.material[k])) return bad("material slot out of range");
             const uint32_t *ms = op.material;
             PtMat m;
             std::memset(&m, 0, sizeof m);
@@ -164,14 +235,14 @@ int derive(pt_ctx *c, const float *data, uint32_t n, std::vector<PtNode> &nodes,
             mats.push_back(m);
         }
     }
-    boxes.resize(c->aabbs.size());
-    for (size_t i = 0; i < c->aabbs.size(); ++i) {
-        const pt_aabb &a = c->aabbs[i];
+    boxes.resize(aabbs.size());
+    for (size_t i = 0; i < aabbs.size(); ++i) {
+        const pt_aabb &a = aabbs[i];
         for (int k = 0; k < 3; ++k)
             if (!in(a.union_position[k]) || !in(a.shape_position[k]) || !in(a.size[k]))
-                return fail(c, PT_ERR_INVALID, "aabb slot out of range");
+                return bad("aabb slot out of range");
         if (!in(a.union_scale) || !in(a.shape_scale) || !in(a.aabb_exaggeration))
-            return fail(c, PT_ERR_INVALID, "aabb slot out of range");
+            return bad("aabb slot out of range");
         float so[3];
         switch (a.so_kind) {
             case PT_SO_SCALAR: so[0] = so[1] = so[2] = data[a.size[0]]; break;
@@ -201,6 +272,8 @@ int derive(pt_ctx *c, const float *data, uint32_t n, std::vector<PtNode> &nodes,
     }
     return PT_OK;
 }
+
+namespace {
 
 }  // namespace
 
@@ -289,8 +362,9 @@ int pt_set_data(pt_ctx *c, const float *data, uint32_t n) {
     std::vector<PtNode> nodes;
     std::vector<PtAabb> boxes;
     std::vector<PtMat> mats;
-    int rc = derive(c, data, n, nodes, boxes, mats);
-    if (rc != PT_OK) return rc;
+    std::string err;
+    int rc = pt_derive(c->ops, c->aabbs, data, n, nodes, boxes, mats, err);
+    if (rc != PT_OK) return fail(c, rc, err);
     HIPCHK(c, hipSetDevice(c->device));
     // stream-ordered upload: in-flight dispatches finish with the old tables
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -307,6 +381,7 @@ int pt_set_data(pt_ctx *c, const float *data, uint32_t n) {
     HIPCHK(c, hipMemcpyAsync(c->d_mats, mats.data(), mats.size() * sizeof(PtMat), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->have_data = true;
+    jit_refresh(c, nodes);
     return PT_OK;
 }
 
@@ -316,6 +391,20 @@ int pt_set_tiles(pt_ctx *c, uint32_t rank, uint32_t nranks) {
     c->rank = rank;
     c->nranks = nranks;
     return pt_resize_clear(c, c->width, c->height);
+}
+
+// Launch one chunk: the scene-specialised wavefront kernel when loaded, else
+// the ahead-of-time kernels (pt_kernel.hip).
+static int launch(pt_ctx *c, PtLaunch &L, bool stats) {
+    if (!pt_use_simple_kernel(L) && c->jit_mod.module) {
+        void *args[] = {&L};
+        HIPCHK(c, hipModuleLaunchKernel(stats ? c->jit_mod.render_stats : c->jit_mod.render, unsigned(L.n_tiles), 1, 1,
+                                        64, 1, 1, 0, c->stream, args, nullptr));
+    } else {
+        pt_launch_render(L, stats, c->stream);
+        HIPCHK(c, hipGetLastError());
+    }
+    return PT_OK;
 }
 
 static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t spp, PtLaunch &L) {
@@ -377,8 +466,7 @@ int pt_dispatch(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t
             Lc.frame0 = int32_t(uint32_t(L.frame0) + done);
             Lc.last_clear0 = int32_t(uint32_t(L.last_clear0) + done);
             if (L.debug != 0 && done + chunk < spp) continue;  // direct stores: only the last frame survives
-            pt_launch_render(Lc, false, c->stream);
-            HIPCHK(c, hipGetLastError());
+            if ((rc = launch(c, Lc, false)) != PT_OK) return rc;
         }
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
@@ -397,10 +485,8 @@ int pt_dispatch_stats(pt_ctx *c, const pt_constants *k, const pt_settings *s, ui
     HIPCHK(c, hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * PT_ST_COUNT, c->stream));
     L.stats = c->d_stats;
     L.write = 0;
-    if (spp > 0 && L.n_tiles > 0) {
-        pt_launch_render(L, true, c->stream);
-        HIPCHK(c, hipGetLastError());
-    }
+    if (spp > 0 && L.n_tiles > 0)
+        if ((rc = launch(c, L, true)) != PT_OK) return rc;
     unsigned long long host[PT_ST_COUNT];
     HIPCHK(c, hipMemcpyAsync(host, c->d_stats, sizeof host, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -502,6 +588,12 @@ int pt_set_option(pt_ctx *c, const char *key, int value) {
         c->kernel = value;
         return PT_OK;
     }
+    if (!std::strcmp(key, "jit")) {
+        if (value != 0 && value != 1) return fail(c, PT_ERR_INVALID, "jit must be 0 or 1");
+        c->jit = value;
+        if (!value) pt_jit_unload(c->jit_mod);  // re-enabled on the next pt_set_data
+        return PT_OK;
+    }
     if (!std::strcmp(key, "shade_batch")) {
         if (value < 1 || value > 64) return fail(c, PT_ERR_INVALID, "shade_batch must be in [1, 64]");
         c->shade_batch = value;
@@ -510,6 +602,18 @@ int pt_set_option(pt_ctx *c, const char *key, int value) {
     return fail(c, PT_ERR_INVALID, std::string("unknown option ") + key);
 }
 
+int pt_get_option(pt_ctx *c, const char *key, double *value) {
+    if (!c || !key || !value) return PT_ERR_INVALID;
+    if (!std::strcmp(key, "jit_active")) *value = c->jit_mod.module ? 1.0 : 0.0;
+    else if (!std::strcmp(key, "jit_seconds")) *value = c->jit_seconds;
+    else if (!std::strcmp(key, "kernel")) *value = c->kernel;
+    else if (!std::strcmp(key, "shade_batch")) *value = c->shade_batch;
+    else return fail(c, PT_ERR_INVALID, std::string("unknown option ") + key);
+    return PT_OK;
+}
+
+const char *pt_jit_log(const pt_ctx *c) { return c ? c->jit_log.c_str() : ""; }
+
 const char *pt_last_error(const pt_ctx *c) { return c ? c->err.c_str() : "null context"; }
 
 void pt_destroy(pt_ctx *c) {
@@ -517,6 +621,7 @@ void pt_destroy(pt_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    pt_jit_unload(c->jit_mod);
     (void)hipFree(c->accum);
     (void)hipFree(c->reduced);
     (void)hipFree(c->d_nodes);

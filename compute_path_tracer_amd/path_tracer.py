@@ -26,7 +26,7 @@ def default_settings() -> N.Settings:
 
 class PathTracer:
     def __init__(self, width: int, height: int, program: Optional[Program] = None, data: Optional[np.ndarray] = None,
-                 device: int = 0, settings: Optional[N.Settings] = None):
+                 device: int = 0, settings: Optional[N.Settings] = None, options: Optional[dict] = None):
         """PathTracer::new (path_tracer.rs:28-60) + the storage texture it binds
         (StorageTexturePackage::new, structs.rs:113-160).  ``width``/``height``
         are the window size; the image is window * settings.scale."""
@@ -40,6 +40,8 @@ class PathTracer:
         ctx = ctypes.c_void_p()
         N.check("pt_create", self._L.pt_create(device, self.size[0], self.size[1], ctypes.byref(ctx)))
         self._ctx = ctx
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
         if program is not None:
             self.remake_pipeline(program)
             self.set_data(program.data if data is None else data)
@@ -124,12 +126,21 @@ class PathTracer:
                                                                   ctypes.byref(self.settings), spp, buf))
         return dict(zip(N.STAT_NAMES, (int(v) for v in buf)))
 
-    KERNELS = {"auto": 0, "simple": 1, "wave": 2}
+    KERNELS = {"auto": 0, "simple": 1, "wave": 2, "jit": 2}
 
     def set_option(self, key: str, value) -> None:
         if key == "kernel" and isinstance(value, str):
             value = self.KERNELS[value]
         self._chk("pt_set_option", self._L.pt_set_option(self._ctx, key.encode(), int(value)))
+
+    def get_option(self, key: str) -> float:
+        v = ctypes.c_double()
+        self._chk("pt_get_option", self._L.pt_get_option(self._ctx, key.encode(), ctypes.byref(v)))
+        return float(v.value)
+
+    def jit_log(self) -> str:
+        raw = self._L.pt_jit_log(self._ctx)
+        return raw.decode() if raw else ""
 
     def set_tiles(self, rank: int, nranks: int) -> None:
         self._chk("pt_set_tiles", self._L.pt_set_tiles(self._ctx, rank, nranks))

@@ -14,8 +14,10 @@
 #ifndef PT_ABI_H
 #define PT_ABI_H
 
+#ifndef __HIPCC_RTC__ /* also embedded in the hipRTC-compiled scene kernels */
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -177,9 +179,21 @@ int pt_last_dispatch_ms(pt_ctx *ctx, float *ms);
 int pt_dispatch_stats(pt_ctx *ctx, const pt_constants *c, const pt_settings *s, uint32_t spp,
                       uint64_t counters[PT_STAT_COUNT]);
 /* Tuning knobs: "kernel" (0 auto, 1 simple one-path-per-lane, 2 wavefront
- * state machine) and "shade_batch" (wavefront kernel: lanes that must wait
- * before a shading pass runs, 1..64).  Results are identical for every value. */
+ * state machine), "shade_batch" (wavefront kernel: lanes that must wait
+ * before a shading pass runs, 1..64) and "jit" (1: per-scene hipRTC build of
+ * the wavefront kernel, compiled at pt_set_data when the topology or an
+ * identity flag changed -- the analogue of remake_pipeline; 0: op-list
+ * interpreter).  Results are bit-identical for every value. */
 int pt_set_option(pt_ctx *ctx, const char *key, int value);
+/* Read back: "jit_active" (1 when the scene-specialised kernel is loaded),
+ * "jit_seconds" (last hipRTC compile time), "kernel", "shade_batch". */
+int pt_get_option(pt_ctx *ctx, const char *key, double *value);
+/* Log of the last failed scene-kernel build ("" if none). */
+const char *pt_jit_log(const pt_ctx *ctx);
+/* Build the scene-specialised kernel for (program, data) with hipRTC without
+ * a device (validation / cache warm-up); *code_bytes = code object size. */
+int pt_jit_compile(const pt_op *ops, uint32_t n_ops, const pt_aabb *aabbs, uint32_t n_aabb, const float *data,
+                   uint32_t n_data, char *log, size_t log_cap, size_t *code_bytes);
 const char *pt_last_error(const pt_ctx *ctx);
 void pt_destroy(pt_ctx *ctx);
 int pt_abi_version(void);

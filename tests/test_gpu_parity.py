@@ -19,14 +19,20 @@ pytestmark = pytest.mark.gpu
 RMS_TOL = 1e-5
 
 
-def _render_pair(ed, w, h, spp, bounces, debug=0, frame=1, last_clear=1, fov=1.0, aspect=None, kernel="auto",
+KERNELS = {"simple": {"kernel": "simple", "jit": 0}, "wave": {"kernel": "wave", "jit": 0},
+           "jit": {"kernel": "wave", "jit": 1}}
+
+
+def _render_pair(ed, w, h, spp, bounces, debug=0, frame=1, last_clear=1, fov=1.0, aspect=None, kernel="jit",
                  shade_batch=None):
     prog = ed.compile(CompData())
     st = N.Settings(debug=debug, bounces=bounces, scale=1.0, fov=fov, aabb=0)
-    pt = PathTracer(w, h, prog, settings=st)
-    pt.set_option("kernel", kernel)
+    opts = dict(KERNELS[kernel])
     if shade_batch:
-        pt.set_option("shade_batch", shade_batch)
+        opts["shade_batch"] = shade_batch
+    pt = PathTracer(w, h, prog, settings=st, options=opts)
+    if kernel == "jit":
+        assert pt.get_option("jit_active") == 1.0, pt.jit_log()
     a = float(np.float32(w) / np.float32(h)) if aspect is None else aspect
     pt.dispatch(N.Constants(time=0.0, frame=frame, aspect=a, last_clear=last_clear), spp)
     gpu = pt.read_image()
@@ -45,7 +51,7 @@ def _report(gpu, ref):
     return rms, exact
 
 
-@pytest.mark.parametrize("kernel", ["simple", "wave"])
+@pytest.mark.parametrize("kernel", ["simple", "wave", "jit"])
 @pytest.mark.parametrize("name,w,h,spp,bounces", [
     ("c1", 256, 256, 1, 1),        # BASELINE config 1 in full
     ("c2", 96, 64, 4, 4),
@@ -61,7 +67,7 @@ def test_parity_path_trace(gpu, name, w, h, spp, bounces, kernel):
     assert exact == 1.0
 
 
-@pytest.mark.parametrize("kernel", ["simple", "wave"])
+@pytest.mark.parametrize("kernel", ["simple", "wave", "jit"])
 @pytest.mark.parametrize("debug", [1, 2, 3])
 def test_parity_debug_views(gpu, debug, kernel):
     gpu_img, ref = _render_pair(scenes.c3_graph32(), 80, 45, 2, 8, debug=debug, kernel=kernel)
@@ -69,11 +75,12 @@ def test_parity_debug_views(gpu, debug, kernel):
     assert rms < RMS_TOL and exact == 1.0
 
 
+@pytest.mark.parametrize("kernel", ["wave", "jit"])
 @pytest.mark.parametrize("shade_batch", [1, 7, 64])
-def test_wave_kernel_schedule_invariance(gpu, shade_batch):
+def test_wave_kernel_schedule_invariance(gpu, shade_batch, kernel):
     """Shading batch size changes the schedule only, never the result; spp
     above the LDS ring size exercises the in-order fold."""
-    gpu_img, ref = _render_pair(scenes.c3_graph32(), 40, 24, 19, 8, kernel="wave", shade_batch=shade_batch)
+    gpu_img, ref = _render_pair(scenes.c3_graph32(), 40, 24, 19, 8, kernel=kernel, shade_batch=shade_batch)
     rms, exact = _report(gpu_img, ref)
     assert exact == 1.0, (shade_batch, rms)
 
@@ -135,6 +142,31 @@ def test_tiles_union_is_full_image(gpu):
     assert np.array_equal(acc.view(np.uint32), ref.view(np.uint32))
 
 
+def test_jit_recompiles_only_on_flag_change(gpu):
+    """Value edits reuse the scene kernel; an identity flag flip (rotation 0 ->
+    non-zero) rebuilds it; results stay exact throughout."""
+    ed = scenes.c2_sphere_box_torus()
+    cd = CompData()
+    prog = ed.compile(cd)
+    st = N.Settings(debug=0, bounces=3, scale=1.0, fov=1.0, aabb=0)
+    pt = PathTracer(40, 30, prog, settings=st, options={"jit": 1})
+    assert pt.get_option("jit_active") == 1.0
+    sph = ed.header_unions[0].children_shapes[1]
+    sph.transform.position.x.set(-0.3)  # value only
+    ed.data_update(cd)
+    pt.set_data(cd.data_array.as_array())
+    assert pt.get_option("jit_active") == 1.0
+    sph.transform.rotation.y.set(0.7)  # rotation about y becomes non-identity
+    ed.data_update(cd)
+    pt.set_data(cd.data_array.as_array())
+    assert pt.get_option("jit_active") == 1.0
+    c = N.Constants(time=0.0, frame=1, aspect=float(np.float32(40) / np.float32(30)), last_clear=1)
+    pt.dispatch(c, 2)
+    gpu_img = pt.read_image()
+    ref = O.OracleScene(ed.rows()).render(40, 30, O.Constants(0.0, 1, c.aspect, 1), O.Settings(0, 3, 1.0, 1.0, 0), 2)
+    assert np.array_equal(gpu_img.view(np.uint32), ref.view(np.uint32))
+
+
 def test_value_update_without_recompile(gpu):
     ed = scenes.c2_sphere_box_torus()
     cd = CompData()
@@ -152,11 +184,12 @@ def test_value_update_without_recompile(gpu):
     assert np.array_equal(gpu_img.view(np.uint32), ref.view(np.uint32))
 
 
-def test_work_counters_match_oracle(gpu):
+@pytest.mark.parametrize("kernel", ["simple", "wave", "jit"])
+def test_work_counters_match_oracle(gpu, kernel):
     ed = scenes.c3_graph32()
     prog = ed.compile(CompData())
     st = N.Settings(debug=0, bounces=8, scale=1.0, fov=1.0, aabb=0)
-    pt = PathTracer(64, 40, prog, settings=st)
+    pt = PathTracer(64, 40, prog, settings=st, options=KERNELS[kernel])
     a = float(np.float32(64) / np.float32(40))
     got = pt.stats(N.Constants(time=0.0, frame=1, aspect=a, last_clear=1), 2)
     _, ct = O.OracleScene(ed.rows()).render(64, 40, O.Constants(0.0, 1, a, 1), O.Settings(0, 8, 1.0, 1.0, 0), 2,
