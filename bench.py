@@ -56,6 +56,20 @@ def algorithmic_flops(st: dict) -> float:
     return float(f)
 
 
+def schedule_metrics(st: dict) -> dict:
+    """SIMD efficiency of the wavefront schedule from the instrumented run."""
+    maps = st["march_steps"] + st["normal_maps"]
+    out = {}
+    if st.get("wave_shapes"):
+        out["map_lane_util"] = round(st["xform_shape"] / (64.0 * st["wave_shapes"]), 4)
+        out["wave_shapes_per_map"] = round(st["wave_shapes"] / max(1, st["wave_maps"]), 3)
+        out["lane_shapes_per_map"] = round(st["xform_shape"] / max(1, maps), 3)
+    if st.get("wave_iters"):
+        out["lane_busy"] = round(1.0 - st["lane_idle"] / (64.0 * st["wave_iters"]), 4)
+        out["maps_per_sample"] = round(maps / max(1, st["samples"]), 2)
+    return out
+
+
 def cpu_baseline(scene, w, h, bounces, threads: int, row_stride: int, spp: int) -> dict:
     from oracle import oracle as O  # test infrastructure: the CPU restatement
 
@@ -203,6 +217,7 @@ def main() -> None:
         "hbm": {"achieved": round(achieved_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "algorithmic_bytes_per_launch": bytes_per_launch},
         "work": st,
+        "schedule": schedule_metrics(st),
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(ed, args.width, args.height, args.bounces, args.cpu_threads,

@@ -161,8 +161,15 @@ __device__ __forceinline__ Hit combine(int32_t how, Hit a, Hit b) {
     return combine_c<PT_COMBINE_SUBTRACTION>(a, b);
 }
 
+// lane-0-of-the-active-set bookkeeping for wave-level counters
+__device__ __forceinline__ bool first_active_lane() {
+    return __builtin_amdgcn_readfirstlane(int(threadIdx.x)) == int(threadIdx.x);
+}
+
 template <bool ST>
 __device__ __forceinline__ void count_shape(Stats<ST> &st, int shape, int how) {
+    if constexpr (ST)
+        if (first_active_lane()) st.add(PT_ST_WAVE_SHAPES);
     st.add(PT_ST_XFORM_SHAPE);
     st.add(PT_ST_SDF_SPHERE + (shape - PT_NODE_SPHERE));
     st.add(how == PT_COMBINE_ASSIGN ? PT_ST_COMB_ASSIGN : (how == PT_COMBINE_UNION ? PT_ST_COMB_UNION : PT_ST_COMB_SUB));

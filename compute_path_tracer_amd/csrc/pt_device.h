@@ -83,6 +83,10 @@ enum {
     PT_ST_COMB_SUB,
     PT_ST_COMB_ASSIGN,
     PT_ST_RR_BREAK,
+    PT_ST_WAVE_MAPS,    // wave-level map() executions (one per wave per call)
+    PT_ST_WAVE_SHAPES,  // wave-level shape evaluations (>= 1 lane passed check[])
+    PT_ST_WAVE_ITERS,   // wavefront kernel loop iterations (per wave)
+    PT_ST_LANE_IDLE,    // lanes without map work in an iteration (wavefront kernel)
     PT_ST_COUNT
 };
 
@@ -115,4 +119,6 @@ struct PtLaunch {
 #define PT_KERNEL_AUTO 0
 #define PT_KERNEL_SIMPLE 1     // one path per lane, reference loop structure
 #define PT_KERNEL_WAVEFRONT 2  // per-lane state machine with job refill
-#define PT_RING 8              // wavefront kernel: in-flight samples per pixel
+#ifndef PT_RING
+#define PT_RING 4              // wavefront kernel: in-flight samples per pixel (power of 2)
+#endif

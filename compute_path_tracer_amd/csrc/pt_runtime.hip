@@ -447,7 +447,7 @@ static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, u
         return v ? std::atoi(v) : 0;
     }();
     L.kernel = c->kernel >= 0 ? c->kernel : env_kernel;
-    L.shade_batch = c->shade_batch > 0 ? c->shade_batch : (env_batch > 0 ? env_batch : 1);
+    L.shade_batch = c->shade_batch > 0 ? c->shade_batch : (env_batch > 0 ? env_batch : 16);
     return PT_OK;
 }
 

@@ -207,12 +207,22 @@ def nested_demo() -> SDFEditor:
     return SDFEditor([outer, top2])
 
 
+def c3_no_aabb() -> SDFEditor:
+    """c3 with every Transform.aabb off (profiling aid: no per-lane culling)."""
+    ed = c3_graph32()
+    for u in ed.header_unions:
+        for sh in u.children_shapes:
+            sh.transform.aabb = False
+    return ed
+
+
 SCENES = {
     "empty": empty,
     "c1": c1_default,
     "c2": c2_sphere_box_torus,
     "c3": c3_graph32,
     "nested": nested_demo,
+    "c3_noaabb": c3_no_aabb,
 }
 
 # BASELINE.json configs -> (scene, width, height, spp, bounces)

@@ -1,10 +1,12 @@
 #!/bin/bash
 # A/B of kernel variants on the bench workload, one process per variant.
+# Variants: env-var sets separated by ';' in AB_VARIANTS.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for v in ${AB_VARIANTS:-"PT_JIT=0 PT_SHADE_BATCH=8" "PT_JIT=1 PT_SHADE_BATCH=1" "PT_JIT=1 PT_SHADE_BATCH=8" "PT_JIT=1 PT_SHADE_BATCH=16"}; do
-  env $v timeout -k 10 300 python bench.py --steps ${AB_STEPS:-3} --warmup 1 --no-cpu-baseline > gpurun_out/ab.tmp 2>&1
+IFS=';' read -ra VARS <<< "${AB_VARIANTS:-PT_JIT=0 PT_SHADE_BATCH=8;PT_JIT=1 PT_SHADE_BATCH=1;PT_JIT=1 PT_SHADE_BATCH=8;PT_JIT=1 PT_SHADE_BATCH=16}"
+for v in "${VARS[@]}"; do
+  env $v timeout -k 10 300 python bench.py --steps ${AB_STEPS:-3} --warmup 1 --no-cpu-baseline ${AB_ARGS:-} > gpurun_out/ab.tmp 2>&1
   rc=$?
   echo "$v rc=$rc $(python -c "import json,sys; d=json.loads(open('gpurun_out/ab.tmp').read().strip().splitlines()[-1]); print(d['value'], d['roofline']['kernel_ms_per_launch'])" 2>/dev/null)" | tee -a gpurun_out/ab.log
   if [ $rc -ne 0 ]; then cat gpurun_out/ab.tmp; exit $rc; fi
