@@ -120,17 +120,15 @@ def main() -> None:
     from compute_path_tracer_amd.path_tracer import PathTracer
     from compute_path_tracer_amd.sdf_editor import CompData
 
+    from compute_path_tracer_amd.distributed import TileSplitRender
+
     ed = scenes.SCENES[args.scene]()
     prog = ed.compile(CompData())
     settings = N.Settings(debug=0, bounces=args.bounces, scale=1.0, fov=1.0, aabb=0)
     pt = PathTracer(args.width, args.height, prog, device=local_rank, settings=settings)
     aspect = float(np.float32(args.width) / np.float32(args.height))
     spp_step = args.spp * world  # weak scaling: each rank owns 1/world of the tiles
-    if world > 1:
-        pt.set_tiles(rank, world)
-        uid = [pt.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        pt.comm_init(world, rank, uid[0])
+    tr = TileSplitRender(pt, rank, world, aspect)
 
     def barrier():
         if dist is not None:
@@ -139,14 +137,9 @@ def main() -> None:
             torch.cuda.synchronize()
             dist.barrier()
 
-    frame = [1]
-
     def step():
-        c = N.Constants(time=0.0, frame=frame[0], aspect=aspect, last_clear=frame[0])
-        pt.dispatch(c, spp_step)
-        frame[0] += spp_step
-        if world > 1:
-            pt.reduce(0)
+        tr.step(args.spp)
+        tr.reduce(0)  # RCCL sum of the tile images onto rank 0 (no-op at world 1)
 
     # algorithmic work per step from the instrumented kernel (outside timing)
     st = pt.stats(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), spp_step)
@@ -172,7 +165,7 @@ def main() -> None:
         dt = float(tt.item())
     if world > 1:
         # per-launch kernel time on this rank (events on the library stream)
-        pt.dispatch(N.Constants(time=0.0, frame=frame[0], aspect=aspect, last_clear=frame[0]), spp_step)
+        tr.step(args.spp)
         kernel_ms.append(pt.last_dispatch_ms())
 
     pixels = args.width * args.height
@@ -218,6 +211,7 @@ def main() -> None:
                 "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "algorithmic_bytes_per_launch": bytes_per_launch},
         "work": st,
         "schedule": schedule_metrics(st),
+        "jit": {"active": bool(pt.get_option("jit_active")), "compile_s": round(pt.get_option("jit_seconds"), 3)},
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(ed, args.width, args.height, args.bounces, args.cpu_threads,

@@ -1,0 +1,81 @@
+"""Multi-GPU rendering: cyclic 8x8-tile ownership + one reduce per render.
+
+Every pixel's sample sequence depends only on (x, y, frame, W, H, scene)
+(rng.glsl:26-36), so rank r rendering the tiles t with t % world == r and
+summing the images (non-owned texels are exactly 0) reproduces the 1-GPU
+image bit for bit.  One process per GPU (torch.distributed launch); the image
+reduce runs over RCCL inside the library (pt_reduce_accum), the 128-byte RCCL
+id travels over the torch process group.  The reference has no multi-GPU path
+(SURVEY.md 2, 8(e)); this is the build's addition.
+
+The orchestration is backend-agnostic: anything with ``set_tiles``,
+``dispatch``, ``comm_unique_id``/``comm_init`` and ``reduce``/``read_reduced``
+(PathTracer on the GPU) can be driven by :class:`TileSplitRender`.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional
+
+import numpy as np
+
+from . import _native as N
+
+
+def env_ranks():
+    """(rank, world, local_rank) from the torch.distributed launcher env."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def torch_broadcast_object(obj, src: int = 0):
+    import torch.distributed as dist
+
+    box = [obj]
+    dist.broadcast_object_list(box, src=src)
+    return box[0]
+
+
+class TileSplitRender:
+    """Progressive render of one image across ``world`` ranks.
+
+    Weak scaling in samples: a step of ``spp`` frames per GPU-share renders
+    ``spp * world`` frames of this rank's 1/world of the tiles, i.e. the same
+    per-GPU work at any world size; frames keep the reference's counters
+    (frame j = frame0 + j, last_clear j = last_clear0 + j, path_tracer.rs:110-111).
+    """
+
+    def __init__(self, renderer, rank: int, world: int, aspect: float,
+                 broadcast: Optional[Callable] = None, frame0: int = 1):
+        self.r = renderer
+        self.rank, self.world = rank, world
+        self.aspect = float(aspect)
+        self.frame = frame0
+        self.last_clear = frame0
+        renderer.set_tiles(rank, world)
+        if world > 1:
+            bcast = broadcast or torch_broadcast_object
+            uid = bcast(renderer.comm_unique_id() if rank == 0 else None)
+            renderer.comm_init(world, rank, uid)
+
+    def constants(self) -> N.Constants:
+        return N.Constants(time=0.0, frame=self.frame, aspect=self.aspect, last_clear=self.last_clear)
+
+    def step(self, spp_per_share: int) -> int:
+        """Render ``spp_per_share * world`` frames of this rank's tiles."""
+        n = spp_per_share * self.world
+        self.r.dispatch(self.constants(), n)
+        self.frame += n
+        self.last_clear += n
+        return n
+
+    def reduce(self, root: int = 0) -> None:
+        if self.world > 1:
+            self.r.reduce(root)
+
+    def image(self, root: int = 0) -> Optional[np.ndarray]:
+        """The assembled image on ``root`` (None elsewhere)."""
+        if self.world == 1:
+            return self.r.read_image()
+        self.r.reduce(root)
+        return self.r.read_reduced() if self.rank == root else None

@@ -114,10 +114,12 @@ def oracle_images():
 
     cases = {
         "oracle_c1_32x32_s2_b1": ("c1", 32, 32, 2, 1, 0),
-        "oracle_c2_24x16_s2_b4": ("c2", 24, 16, 2, 4, 0),
-        "oracle_c3_16x12_s1_b8": ("c3", 16, 12, 1, 8, 0),
-        "oracle_nested_16x16_s1_b4": ("nested", 16, 16, 1, 4, 0),
-        "oracle_c3_dbg1_16x12": ("c3", 16, 12, 1, 8, 1),
+        "oracle_c2_16x12_s2_b4": ("c2", 16, 12, 2, 4, 0),
+        "oracle_c3_8x6_s1_b8": ("c3", 8, 6, 1, 8, 0),
+        "oracle_nested_8x8_s1_b4": ("nested", 8, 8, 1, 4, 0),
+        "oracle_c3_dbg1_8x6": ("c3", 8, 6, 1, 8, 1),
+        "oracle_c3_dbg2_8x6": ("c3", 8, 6, 1, 8, 2),
+        "oracle_c3_dbg3_8x6": ("c3", 8, 6, 1, 8, 3),
     }
     meta = {}
     for name, (sc, w, h, spp, b, dbg) in cases.items():

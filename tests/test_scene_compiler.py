@@ -1,0 +1,170 @@
+"""The scene compiler (pt_compile_scene) and the editor mirror.  No GPU."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+from compute_path_tracer_amd import _native as N
+from compute_path_tracer_amd import scenes
+from compute_path_tracer_amd.sdf_editor import (CompData, SDFEditor, Shape, Shapes, Union, UnionType, compile_rows,
+                                                nodes_to_ctypes)
+from oracle import oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _captured_scene() -> SDFEditor:
+    """The tree behind shader_out/test_compute.glsl: header union "BOX"
+    (Subtraction, two cubes, aabb off) and "stuffs" (Union: sphere, cube,
+    sphere, sphere, cube, aabb on)."""
+    box = Union(UnionType.SUBTRACTION)
+    box.name = "BOX"
+    for _ in range(2):
+        s = Shape(Shapes.CUBE)
+        s.transform.aabb = False
+        box.children_shapes.append(s)
+    stuffs = Union(UnionType.UNION)
+    stuffs.name = "stuffs"
+    for k in (Shapes.SPHERE, Shapes.CUBE, Shapes.SPHERE, Shapes.SPHERE, Shapes.CUBE):
+        stuffs.children_shapes.append(Shape(k))
+    return SDFEditor([box, stuffs])
+
+
+def test_topology_matches_captured_compiler_output():
+    fx = json.load(open(os.path.join(GOLD, "shader_out_topology.json")))
+    prog = _captured_scene().compile(CompData())
+    assert prog.n_check == fx["n_check"] == 7
+    assert len(prog.data) == 214  # data[0..213]
+    ops = prog.op_dicts()
+    i = 0
+    comb = {"assign": N.PT_COMBINE_ASSIGN, "opUnion": N.PT_COMBINE_UNION, "opSubtraction": N.PT_COMBINE_SUBTRACTION}
+    for u in fx["unions"]:
+        b = ops[i]
+        assert b["opcode"] == N.PT_OP_UNION_BEGIN
+        assert b["scale"] == u["scale"] == u["scale_again"] and b["position"] == u["position"]
+        assert b["rotation"] == u["rotation"]
+        i += 1
+        for s in u["shapes"]:
+            o = ops[i]
+            assert o["opcode"] == N.PT_OP_SHAPE
+            assert o["shape"] == (N.PT_NODE_CUBE if s["kind"] == "Cube" else N.PT_NODE_SPHERE)
+            assert o["scale"] == s["scale"] == s["scale_again"] == s["finalise_scale"]
+            assert o["position"] == s["position"] and o["rotation"] == s["rotation"]
+            nsz = len(s["size"])
+            assert o["size"][:nsz] == s["size"]
+            assert o["material"] == s["material"]
+            assert o["check"] == (-1 if s["check"] is None else s["check"])
+            assert o["combine"] == comb[s["combine"]]
+            i += 1
+        e = ops[i]
+        assert e["opcode"] == N.PT_OP_UNION_END and e["combine"] == comb[u["combine"]]
+        i += 1
+    assert i == prog.n_ops
+    boxes = {a["back"]: a for a in prog.aabb_dicts()}
+    for b in fx["bounds"]:
+        if not b["enabled"]:
+            assert b["back"] not in boxes
+            continue
+        a = boxes[b["back"]]
+        assert a["union_position"] == b["union_position"] and a["shape_position"] == b["shape_position"]
+        assert a["union_scale"] == b["union_scale"] and a["shape_scale"] == b["shape_scale"]
+        assert a["aabb_exaggeration"] == b["aabb_exaggeration"]
+        so = b["size"]
+        assert a["size"][:len(so)] == so
+        assert a["so_kind"] == (N.PT_SO_SCALAR if len(so) == 1 else N.PT_SO_VEC3)
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "nested", "empty"])
+def test_product_compiler_matches_oracle_restatement(name):
+    ed = scenes.SCENES[name]()
+    rows = ed.rows()
+    prog = ed.compile(CompData())
+    osc = O.OracleScene(rows)
+    assert np.array_equal(prog.data.view(np.uint32), osc.data().view(np.uint32))
+    assert prog.n_check == osc.n_check
+    shapes = [o for o in prog.op_dicts() if o["opcode"] == N.PT_OP_SHAPE]
+    si = 0
+    for i, r in enumerate(rows):
+        slots, chk, bidx = osc.node_slots(i)
+        if r["kind"] == N.PT_NODE_UNION:
+            continue
+        o = shapes[si]
+        si += 1
+        assert [o["scale"], *o["position"], *o["rotation"], o["aabb_exaggeration"]] == slots[:8]
+        nsz = {1: 1, 2: 3, 3: 2, 4: 1}[r["kind"]]
+        assert o["size"][:nsz] == slots[8:8 + nsz]
+        assert o["material"] == slots[11:29]
+        assert o["check"] == chk
+    boxes = prog.aabb_dicts()
+    assert sorted(a["back"] for a in boxes) == sorted(
+        osc.node_slots(i)[2] for i, r in enumerate(rows) if r["kind"] != 0 and r["aabb"] and osc.node_slots(i)[2] >= 0)
+
+
+def test_nested_quirks():
+    """child unions combine first and the index-0 shape
+    overwrites them; map() check[] indices run DFS over all shapes while
+    bounds() only numbers the header unions' direct shapes."""
+    prog = scenes.nested_demo().compile(CompData())
+    ops = prog.op_dicts()
+    # outer: BEGIN, inner BEGIN, deeper BEGIN, c, END, a, b, END, d(assign!), e, END
+    seq = [(o["opcode"], o["combine"]) for o in ops]
+    assert seq[:11] == [(0, 0), (0, 0), (0, 0), (1, 0), (2, 2), (1, 0), (1, 2), (2, 1), (1, 0), (1, 1), (2, 1)]
+    checks = [o["check"] for o in ops if o["opcode"] == N.PT_OP_SHAPE]
+    assert checks == [0, 1, 2, -1, -1, -1]  # d, e (aabb off), lamp (aabb off)
+    assert sorted(a["back"] for a in prog.aabb_dicts()) == []  # d/e/lamp are the only bounds() shapes
+
+
+def test_compile_errors_and_two_call_pattern():
+    L = N.lib()
+    ed = SDFEditor([Union()])
+    ed.header_unions[0].children_shapes.append(Shape(Shapes.PLANE))
+    with pytest.raises(N.NativeError) as e:
+        ed.compile(CompData())
+    assert e.value.code == N.PT_ERR_UNSUPPORTED
+    rows = scenes.c2_sphere_box_torus().rows()
+    bad = [dict(r) for r in rows]
+    bad[1]["parent"] = 5  # parent after child
+    with pytest.raises(N.NativeError):
+        compile_rows(bad)
+    top_shape = [dict(rows[1], parent=-1)]
+    with pytest.raises(N.NativeError):
+        compile_rows(top_shape)
+    nodes = nodes_to_ctypes(rows)
+    n_ops, n_aabb, n_data, n_check = (ctypes.c_uint32() for _ in range(4))
+    small = (N.Op * 1)()
+    rc = L.pt_compile_scene(nodes, len(rows), small, 1, ctypes.byref(n_ops), None, 0, ctypes.byref(n_aabb), None, 0,
+                            ctypes.byref(n_data), ctypes.byref(n_check))
+    assert rc == N.PT_ERR_SIZE and n_ops.value == 12 and n_data.value == 193 and n_check.value == 6
+
+
+def test_editor_json_round_trip_and_refresh():
+    ed = scenes.c3_graph32()
+    cd = CompData()
+    prog = ed.compile(cd)
+    s = ed.dumps()
+    ed2 = SDFEditor.loads(s)
+    assert ed2.dumps() == s
+    cd2 = CompData()
+    prog2 = ed2.compile(cd2)
+    assert np.array_equal(prog.data, prog2.data)
+    # value-only edit: refresh writes the same slot the compiler allocated
+    u = ed.header_unions[1]
+    f = u.children_shapes[3].transform.position.y
+    slot = cd.data_array.seen[f.hash]
+    f.set(0.125)
+    ed.data_update(cd)
+    assert cd.data_array.data[slot] == np.float32(0.125)
+    # the recompiled program allocates identical slots with the new value
+    prog3 = ed.compile(CompData())
+    assert np.array_equal(prog3.data, cd.data_array.as_array())
+
+
+def test_default_editor_scene():
+    """SDFEditor::new (sdf_editor.rs:20-33): one union + unit sphere, 36 floats."""
+    ed = SDFEditor()
+    prog = ed.compile(CompData())
+    assert len(prog.data) == 36 and prog.data[0] == np.float32(6969.69)
+    assert prog.n_ops == 3 and prog.n_aabb == 1 and prog.n_check == 1
+    assert prog.data[8] == np.float32(1.3)  # aabb_exaggeration default
