@@ -70,6 +70,27 @@ def schedule_metrics(st: dict) -> dict:
     return out
 
 
+def profiled_traffic(config: dict):
+    """HBM bytes per launch of the hot kernel from the newest committed
+    rocprofv3 PMC summary (profiles/*_pmc.json, scripts/summarize_profile.py)
+    taken on this same workload; None if there is none."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        cfg = d.get("bench_config") or {}
+        keys = ("width", "height", "bounces", "spp_per_step")
+        if all(cfg.get(k) == config.get(k) for k in keys) and cfg.get("workload") == config.get("workload"):
+            hb = d.get("derived", {}).get("hbm_bytes_per_launch")
+            if hb:
+                best = (hb, os.path.relpath(f, ROOT))
+    return best
+
+
 def cpu_baseline(scene, w, h, bounces, threads: int, row_stride: int, spp: int) -> dict:
     from oracle import oracle as O  # test infrastructure: the CPU restatement
 
@@ -99,8 +120,8 @@ def main() -> None:
     ap.add_argument("--scene", default="c3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-row-stride", type=int, default=8)
-    ap.add_argument("--cpu-spp", type=int, default=2)
+    ap.add_argument("--cpu-row-stride", type=int, default=1)
+    ap.add_argument("--cpu-spp", type=int, default=6)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -204,6 +225,7 @@ def main() -> None:
                    "spp_per_step": args.spp * world, "parallelism": f"tiles{world}"},
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_TFLOPS, 4), "traffic": None,
+                     "traffic_source": None,
                      "algorithmic_flops_per_sample": round(flops_per_launch / max(1, st["samples"]), 1),
                      "frac_nonpacked": round(achieved_tf / PEAK_F32_TFLOPS_NONPACKED, 4),
                      "kernel_ms_per_launch": round(k_ms, 3)},
@@ -213,6 +235,11 @@ def main() -> None:
         "schedule": schedule_metrics(st),
         "jit": {"active": bool(pt.get_option("jit_active")), "compile_s": round(pt.get_option("jit_seconds"), 3)},
     }
+    tr_prof = profiled_traffic(out["config"])
+    if tr_prof is not None:
+        out["roofline"]["traffic"] = tr_prof[0]
+        out["roofline"]["traffic_source"] = f"{tr_prof[1]} (2*FETCH_SIZE+WRITE_SIZE, KiB->B, per launch)"
+        out["hbm"]["measured_bytes_per_launch"] = tr_prof[0]
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(ed, args.width, args.height, args.bounces, args.cpu_threads,
                                            args.cpu_row_stride, args.cpu_spp)

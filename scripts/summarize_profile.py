@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/profile.sh run (gpurun_out/prof_<tag>) into profiles/.
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats),
+profiles/<tag>_pmc.json (per-launch counters of the hot kernel and derived
+metrics) and profiles/<tag>_summary.md.
+
+HBM bytes per launch follow MI355X_MICROARCH.md "HBM": FETCH_SIZE reads
+exactly half of a wide coalesced stream on gfx950 (16 B/lane loads, which is
+what the kernel's float4 texel load is), so bytes = 2*FETCH_SIZE*1024 +
+WRITE_SIZE*1024 (WRITE_SIZE is exact for 16 B/lane stores); each counter from
+its own pass.
+"""
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOT = ("pt_wave_jit", "pt_wave_kernel", "pt_render_kernel")
+
+
+def hot_name(name: str) -> bool:
+    return any(name.startswith(h) and "stats" not in name and "<true>" not in name for h in HOT)
+
+
+def main(tag: str, src: str = None) -> None:
+    src = src or os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    ks = os.path.join(src, "kt", "kt_kernel_stats.csv")
+    shutil.copy(ks, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    stats = list(csv.DictReader(open(ks)))
+    bench_line = None
+    for line in open(os.path.join(src, "kt_bench.log")):
+        if line.startswith("{"):
+            bench_line = json.loads(line)
+    counters, launches = {}, {}
+    meta = {}
+    for f in sorted(glob.glob(os.path.join(src, "pmc*", "pmc_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            if not hot_name(r["Kernel_Name"]):
+                continue
+            k = r["Counter_Name"]
+            counters[k] = counters.get(k, 0.0) + float(r["Counter_Value"])
+            launches.setdefault(k, set()).add(r["Dispatch_Id"])
+            meta = {"kernel": r["Kernel_Name"], "vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
+                    "lds_bytes": int(r["LDS_Block_Size"]), "grid": int(r["Grid_Size"]),
+                    "workgroup": int(r["Workgroup_Size"])}
+    per_launch = {k: v / max(1, len(launches[k])) for k, v in counters.items()}
+    d = {}
+    c = per_launch
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        d["hbm_bytes_per_launch"] = 2.0 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
+    if "SQ_THREAD_CYCLES_VALU" in c and c.get("SQ_ACTIVE_INST_VALU"):
+        d["valu_lane_utilization"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
+    if c.get("GRBM_GUI_ACTIVE") and c.get("SQ_INSTS_VALU"):
+        cyc = c["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs
+        d["gpu_cycles"] = cyc
+        d["valu_issue_per_simd_cycle"] = c["SQ_INSTS_VALU"] / (1024.0 * cyc)
+        d["valu_issue_frac_of_peak"] = d["valu_issue_per_simd_cycle"] / 0.5  # wave64 VALU = 2 cycles on SIMD32
+        d["salu_per_valu"] = c.get("SQ_INSTS_SALU", 0.0) / c["SQ_INSTS_VALU"]
+    if c.get("SQ_WAVE_CYCLES"):
+        tot = c["SQ_WAVE_CYCLES"]
+        d["wave_time_active"] = c.get("SQ_ACTIVE_INST_ANY", 0.0) / tot
+        d["wave_time_wait_issue"] = c.get("SQ_WAIT_INST_ANY", 0.0) / tot
+        d["wave_time_waitcnt"] = c.get("SQ_WAIT_ANY", 0.0) / tot
+    ktime = None
+    for r in stats:
+        if hot_name(r["Name"]):
+            ktime = float(r["AverageNs"]) * 1e-9
+    if ktime and "hbm_bytes_per_launch" in d:
+        d["hbm_gbs_measured"] = d["hbm_bytes_per_launch"] / ktime / 1e9
+    out = {"tag": tag, "kernel": meta, "per_launch_counters": per_launch, "derived": d,
+           "kernel_avg_s_kernel_trace": ktime,
+           "bench_config": bench_line["config"] if bench_line else None,
+           "bench_value": bench_line["value"] if bench_line else None,
+           "bench_kernel_ms_hip_events": bench_line["roofline"]["kernel_ms_per_launch"] if bench_line else None}
+    with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    lines = [f"# rocprofv3 summary `{tag}`", "",
+             f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py {bench_line['steps'] if bench_line else ''}`"
+             " (see scripts/profile.sh); PMC passes one counter group each.", "",
+             "## Kernel stats", "", "| kernel | calls | avg ms | % |", "|---|---|---|---|"]
+    for r in stats:
+        lines.append(f"| {r['Name']} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | {float(r['Percentage']):.2f} |")
+    lines += ["", f"HIP-event time of the same kernel inside bench.py: "
+                  f"{out['bench_kernel_ms_hip_events']} ms per launch", "",
+              "## Hot kernel counters (per launch)", "", f"kernel: {meta}", ""]
+    for k, v in sorted(per_launch.items()):
+        lines.append(f"- {k}: {v:.6g}")
+    lines += ["", "## Derived", ""]
+    for k, v in d.items():
+        lines.append(f"- {k}: {v:.6g}")
+    with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print(json.dumps(out["derived"], indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
