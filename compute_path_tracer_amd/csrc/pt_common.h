@@ -105,14 +105,14 @@ __device__ __forceinline__ void xform(const PtNode &n, float &x, float &y, float
 template <int K>
 __device__ __forceinline__ float sdf_k(const PtNode &n, float x, float y, float z) {
     if constexpr (K == PT_NODE_SPHERE) {
-        return sqrtf(x * x + y * y + z * z) - n.size[0];
+        return pt_sqrt(x * x + y * y + z * z) - n.size[0];
     } else if constexpr (K == PT_NODE_CUBE) {
         const float qx = fabsf(x) - n.size[0], qy = fabsf(y) - n.size[1], qz = fabsf(z) - n.size[2];
         const float mx = pt_gmax(qx, 0.0f), my = pt_gmax(qy, 0.0f), mz = pt_gmax(qz, 0.0f);
-        return sqrtf(mx * mx + my * my + mz * mz) + pt_gmin(pt_gmax(qx, pt_gmax(qy, qz)), 0.0f);
+        return pt_sqrt(mx * mx + my * my + mz * mz) + pt_gmin(pt_gmax(qx, pt_gmax(qy, qz)), 0.0f);
     } else if constexpr (K == PT_NODE_TORUS) {
-        const float qx = sqrtf(x * x + z * z) - n.size[0];
-        return sqrtf(qx * qx + y * y) - n.size[1];
+        const float qx = pt_sqrt(x * x + z * z) - n.size[0];
+        return pt_sqrt(qx * qx + y * y) - n.size[1];
     } else {  // PT_NODE_OCTAHEDRON
         const float s = n.size[0];
         const float ax = fabsf(x), ay = fabsf(y), az = fabsf(z);
@@ -129,7 +129,7 @@ __device__ __forceinline__ float sdf_k(const PtNode &n, float x, float y, float 
         }
         const float k = pt_gmin(pt_gmax(0.5f * (q2 - q1 + s), 0.0f), s);
         const float vy = q1 - s + k, vz = q2 - k;
-        return sqrtf(q0 * q0 + vy * vy + vz * vz);
+        return pt_sqrt(q0 * q0 + vy * vy + vz * vz);
     }
 }
 __device__ __forceinline__ float sdf(const PtNode &n, float x, float y, float z) {

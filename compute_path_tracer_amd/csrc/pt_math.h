@@ -22,9 +22,14 @@ typedef __hip_internal::size_t size_t;
 
 #define PT_HD __host__ __device__ __forceinline__
 
-// GLSL 4.50 8.3: min(x, y) = y < x ? y : x;  max(x, y) = x < y ? y : x.
-PT_HD float pt_gmin(float x, float y) { return (y < x) ? y : x; }
-PT_HD float pt_gmax(float x, float y) { return (x < y) ? y : x; }
+// GLSL min/max/clamp.  naga lowers them to SPIR-V GLSL.std.450 FMin/FMax/
+// FClamp, which GPU drivers implement with the hardware min/max; on gfx950
+// that is v_min_f32/v_max_f32 = IEEE-754 minNum/maxNum (a NaN operand yields
+// the other operand; -0 < +0).  The contract adopts exactly
+// that; oracle/pt_oracle.c spells it out bit for bit and the device self-test
+// (pt_selftest) checks the hardware against it.
+PT_HD float pt_gmin(float x, float y) { return fminf(x, y); }
+PT_HD float pt_gmax(float x, float y) { return fmaxf(x, y); }
 
 // rng.glsl:1-9
 PT_HD uint32_t pt_wang_hash(uint32_t &seed) {
@@ -85,11 +90,30 @@ PT_HD void pt_sincos(float x, float &s, float &c) {
     }
 }
 
+// Correctly rounded f32 sqrt.  Same result as the compiler's IEEE sqrtf
+// lowering (v_sqrt_f32 + the two-neighbour FMA correction): for inputs below
+// 2^-96 (where that lowering rescales) the wave takes the full sqrtf; zeros,
+// +inf and NaN fall out of the correction unchanged.  Verified against sqrtf
+// for all 2^32 inputs by pt_selftest / tests/test_gpu_selftest.py.
+PT_HD float pt_sqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    if (__builtin_expect(__ballot(x < 0x1p-96f) != 0ull, 0)) return sqrtf(x);
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __int_as_float(__float_as_int(s) - 1);
+    const float su = __int_as_float(__float_as_int(s) + 1);
+    float r = fmaf(-sd, s, x) <= 0.0f ? sd : s;
+    r = fmaf(-su, s, x) > 0.0f ? su : r;
+    return r;
+#else
+    return sqrtf(x);
+#endif
+}
+
 struct pt_f3 {
     float x, y, z;
 };
 PT_HD float pt_dot(pt_f3 a, pt_f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-PT_HD float pt_length(pt_f3 a) { return sqrtf(pt_dot(a, a)); }
+PT_HD float pt_length(pt_f3 a) { return pt_sqrt(pt_dot(a, a)); }
 // GLSL normalize(v) = v / length(v)
 PT_HD pt_f3 pt_normalize(pt_f3 a) {
     float l = pt_length(a);

@@ -198,6 +198,20 @@ const char *pt_last_error(const pt_ctx *ctx);
 void pt_destroy(pt_ctx *ctx);
 int pt_abi_version(void);
 
+/* Device arithmetic probes for the semantics contract (tests only):
+ * out[i] = op(a[i], b[i]) computed by the kernels' own device functions. */
+#define PT_MATH_MAX 0
+#define PT_MATH_MIN 1
+#define PT_MATH_SQRT 2   /* the kernels' fast correctly rounded sqrt */
+#define PT_MATH_SQRTF 3  /* the compiler's IEEE sqrtf */
+#define PT_MATH_SIN 4
+#define PT_MATH_COS 5
+#define PT_MATH_DIV 6
+#define PT_MATH_FMA 7    /* fmaf(a, b, 1) */
+int pt_device_math(int hip_device, int op, const float *a, const float *b, float *out, uint32_t n);
+/* The kernels' sqrt vs IEEE sqrtf over all 2^32 inputs (NaN payloads aside). */
+int pt_check_sqrt_exhaustive(int hip_device, uint64_t *mismatches, uint32_t *first_bad);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,9 +23,24 @@ static const float PI = 3.14159265359f;
 #define PI2 (2.0f * PI)
 #define MAXHIT_D 10000.0f /* sdf_editor.rs:193 */
 
-/* GLSL 4.50 sec. 8.3: min(x,y) = y < x ? y : x ; max(x,y) = x < y ? y : x */
-static inline float gmin(float x, float y) { return (y < x) ? y : x; }
-static inline float gmax(float x, float y) { return (x < y) ? y : x; }
+/* GLSL min/max: naga emits SPIR-V GLSL.std.450 FMin/FMax, which drivers run
+ * on the hardware min/max (gfx950 v_min/v_max_f32 = IEEE-754 minNum/maxNum:
+ * a NaN operand yields the other operand, -0 < +0).  Spelled out here so the
+ * result does not depend on the host libm. */
+static inline float gmin(float x, float y)
+{
+    if (x != x) return y;
+    if (y != y) return x;
+    if (x == 0.0f && y == 0.0f) return (signbit(x) || signbit(y)) ? -0.0f : 0.0f;
+    return (y < x) ? y : x;
+}
+static inline float gmax(float x, float y)
+{
+    if (x != x) return y;
+    if (y != y) return x;
+    if (x == 0.0f && y == 0.0f) return (signbit(x) && signbit(y)) ? -0.0f : 0.0f;
+    return (x < y) ? y : x;
+}
 static inline float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
 static inline float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 static inline float length3(const float a[3]) { return sqrtf(dot3(a, a)); }
@@ -506,6 +521,12 @@ static void get_mat(const pto_scene *s, int32_t id, mat_t *m)
     m->rough = D(sl[11]);
 }
 
+/* Optional segment log (analysis aid, single-threaded renders only). */
+static pto_segment *g_seglog = NULL;
+static int g_seglog_cap = 0, g_seglog_n = 0;
+void pto_set_segment_log(pto_segment *buf, int cap) { g_seglog = buf; g_seglog_cap = cap; g_seglog_n = 0; }
+int pto_segment_log_count(void) { return g_seglog_n; }
+
 static void path_trace(const pto_scene *s, const pto_settings *st, ray_t ray, uint32_t rng, uint8_t *check,
                        float out[3], pto_counters *ct) /* test_compute.glsl:91-166 */
 {
@@ -517,7 +538,18 @@ static void path_trace(const pto_scene *s, const pto_settings *st, ray_t ray, ui
         if (ct) ct->segments++;
         float t;
         int32_t mid;
+        uint64_t steps0 = ct ? ct->march_steps : 0;
         cast_ray(s, &ray, check, &t, &mid, ct);
+        if (g_seglog && g_seglog_n < g_seglog_cap) {
+            pto_segment *sg = &g_seglog[g_seglog_n++];
+            for (int k = 0; k < 3; k++) { sg->ro[k] = ray.ro[k]; sg->rd[k] = ray.rd[k]; }
+            sg->mask[0] = sg->mask[1] = 0;
+            for (int k = 0; k < s->ncheck && k < 128; k++)
+                if (check[k]) sg->mask[k >> 6] |= 1ull << (k & 63);
+            sg->seg = i;
+            sg->steps = ct ? (int32_t)(ct->march_steps - steps0) : -1;
+            sg->hit = t <= FP;
+        }
         if (t > FP) break;
         float hp[3] = {ray.ro[0] + ray.rd[0] * t, ray.ro[1] + ray.rd[1] * t, ray.ro[2] + ray.rd[2] * t};
         float n[3];

@@ -113,6 +113,12 @@ void pto_render(const pto_scene *s, float *image, int w, int h,
                 int rank, int nranks, int row_stride, int nthreads,
                 pto_counters *counters);
 
+/* Analysis aid: log every path segment (ray, check mask, march steps) of
+ * subsequent single-threaded renders into buf (counters must be requested). */
+typedef struct { float ro[3], rd[3]; uint64_t mask[2]; int32_t seg, steps, hit, pad; } pto_segment;
+void pto_set_segment_log(pto_segment *buf, int cap);
+int pto_segment_log_count(void);
+
 #ifdef __cplusplus
 }
 #endif

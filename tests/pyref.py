@@ -46,10 +46,26 @@ def fmaf(a, b, c) -> np.float32:
 
 
 def gmin(x, y):
+    """IEEE-754 minNum with -0 < +0 (SPIR-V FMin on AMD hardware)."""
+    x, y = F(x), F(y)
+    if np.isnan(x):
+        return y
+    if np.isnan(y):
+        return x
+    if x == 0 and y == 0:
+        return F(-0.0) if (np.signbit(x) or np.signbit(y)) else F(0.0)
     return y if y < x else x
 
 
 def gmax(x, y):
+    """IEEE-754 maxNum with -0 < +0 (SPIR-V FMax on AMD hardware)."""
+    x, y = F(x), F(y)
+    if np.isnan(x):
+        return y
+    if np.isnan(y):
+        return x
+    if x == 0 and y == 0:
+        return F(-0.0) if (np.signbit(x) and np.signbit(y)) else F(0.0)
     return y if x < y else x
 
 

@@ -1,0 +1,72 @@
+"""Device arithmetic against the semantics contract."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+
+import pyref
+from compute_path_tracer_amd import _native as N
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(op, a, b=None):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b if b is not None else np.zeros_like(a), np.float32)
+    out = np.empty_like(a)
+    fp = ctypes.POINTER(ctypes.c_float)
+    rc = N.lib().pt_device_math(0, N.PT_MATH[op], a.ctypes.data_as(fp), b.ctypes.data_as(fp), out.ctypes.data_as(fp),
+                                a.size)
+    assert rc == N.PT_OK
+    return out
+
+
+SPECIAL = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 3.4e38, 0.5, -2.5],
+                   np.float32)
+
+
+@pytest.mark.parametrize("op", ["max", "min"])
+def test_min_max_are_ieee_maxnum_minnum(gpu, op):
+    a, b = np.meshgrid(SPECIAL, SPECIAL)
+    a, b = a.ravel(), b.ravel()
+    got = dev(op, a, b)
+    f = pyref.gmax if op == "max" else pyref.gmin
+    want = np.array([f(x, y) for x, y in zip(a, b)], np.float32)
+    nan = np.isnan(got) & np.isnan(want)
+    assert np.array_equal(got.view(np.uint32)[~nan], want.view(np.uint32)[~nan])
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+
+
+def test_sqrt_fast_path_equals_ieee_sqrt_for_all_inputs(gpu):
+    bad, first = ctypes.c_uint64(), ctypes.c_uint32()
+    assert N.lib().pt_check_sqrt_exhaustive(0, ctypes.byref(bad), ctypes.byref(first)) == N.PT_OK
+    assert bad.value == 0, hex(first.value)
+
+
+def test_sqrt_and_div_correctly_rounded(gpu):
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(0, 1e4, 100000), rng.uniform(0, 1e-30, 1000), SPECIAL]).astype(np.float32)
+    y = np.concatenate([rng.uniform(-10, 10, 100000), rng.uniform(1e-3, 1, 1000), SPECIAL[::-1]]).astype(np.float32)
+    with np.errstate(all="ignore"):
+        for op, want in (("sqrt", np.sqrt(x)), ("sqrtf", np.sqrt(x)), ("div", x / y)):
+            got = dev(op, x, y)
+            ok = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+            assert ok.all(), (op, x[~ok][:4], y[~ok][:4])
+
+
+def test_sincos_matches_oracle(gpu):
+    x = np.concatenate([np.linspace(-50, 50, 20001), [0.0, -0.0, 6.2831855, 16777216.0, 2e7]]).astype(np.float32)
+    s, c = dev("sin", x), dev("cos", x)
+    for i in range(0, x.size, 97):
+        assert np.float32(O.sin(float(x[i]))).view(np.uint32) == s[i:i + 1].view(np.uint32)[0] or \
+            (math.isnan(s[i]) and math.isnan(O.sin(float(x[i]))))
+        assert np.float32(O.cos(float(x[i]))).view(np.uint32) == c[i:i + 1].view(np.uint32)[0] or \
+            (math.isnan(c[i]) and math.isnan(O.cos(float(x[i]))))
+
+
+def test_fma_is_fused(gpu):
+    a = np.float32(1.0000001)
+    got = dev("fma", np.array([a], np.float32), np.array([a], np.float32))[0]
+    assert got == pyref.fmaf(a, a, np.float32(1.0))
