@@ -66,6 +66,8 @@ def schedule_metrics(st: dict) -> dict:
         out["lane_shapes_per_map"] = round(st["xform_shape"] / max(1, maps), 3)
     if st.get("wave_iters"):
         out["lane_busy"] = round(1.0 - st["lane_idle"] / (64.0 * st["wave_iters"]), 4)
+        out["idle_shade"] = round(st["idle_shade"] / (64.0 * st["wave_iters"]), 4)
+        out["idle_free"] = round(st["idle_free"] / (64.0 * st["wave_iters"]), 4)
         out["maps_per_sample"] = round(maps / max(1, st["samples"]), 2)
     return out
 

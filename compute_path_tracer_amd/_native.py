@@ -27,11 +27,11 @@ PT_OP_UNION_BEGIN, PT_OP_SHAPE, PT_OP_UNION_END = 0, 1, 2
 PT_COMBINE_ASSIGN, PT_COMBINE_UNION, PT_COMBINE_SUBTRACTION = 0, 1, 2
 PT_SO_SCALAR, PT_SO_VEC3, PT_SO_ONE, PT_SO_TORUS = 0, 1, 2, 3
 PT_COMM_ID_BYTES = 128
-PT_STAT_COUNT = 20
+PT_STAT_COUNT = 24
 STAT_NAMES = (
     "samples", "segments", "march_steps", "normal_maps", "shaded", "aabb_tests", "xform_union", "xform_shape",
     "sdf_sphere", "sdf_cube", "sdf_torus", "sdf_octahedron", "comb_union", "comb_sub", "comb_assign", "rr_break",
-    "wave_maps", "wave_shapes", "wave_iters", "lane_idle",
+    "wave_maps", "wave_shapes", "wave_iters", "lane_idle", "idle_shade", "idle_free", "reserved0", "reserved1",
 )
 
 SYMBOLS = (

@@ -87,6 +87,8 @@ enum {
     PT_ST_WAVE_SHAPES,  // wave-level shape evaluations (>= 1 lane passed check[])
     PT_ST_WAVE_ITERS,   // wavefront kernel loop iterations (per wave)
     PT_ST_LANE_IDLE,    // lanes without map work in an iteration (wavefront kernel)
+    PT_ST_IDLE_SHADE,   //   ... of which waiting for a shading pass
+    PT_ST_IDLE_FREE,    //   ... of which without a job (pool drained / ring full)
     PT_ST_COUNT
 };
 

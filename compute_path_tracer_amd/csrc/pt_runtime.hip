@@ -476,7 +476,7 @@ int pt_dispatch(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t
 
 int pt_dispatch_stats(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t spp,
                       uint64_t counters[PT_STAT_COUNT]) {
-    static_assert(PT_STAT_COUNT == PT_ST_COUNT, "stat count");
+    static_assert(PT_STAT_COUNT >= PT_ST_COUNT, "stat count");
     PtLaunch L;
     int rc = make_launch(c, k, s, spp, L);
     if (rc != PT_OK) return rc;
@@ -490,7 +490,7 @@ int pt_dispatch_stats(pt_ctx *c, const pt_constants *k, const pt_settings *s, ui
     unsigned long long host[PT_ST_COUNT];
     HIPCHK(c, hipMemcpyAsync(host, c->d_stats, sizeof host, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; i < PT_ST_COUNT; ++i) counters[i] = host[i];
+    for (int i = 0; i < PT_STAT_COUNT; ++i) counters[i] = i < PT_ST_COUNT ? host[i] : 0;
     return PT_OK;
 }
 
