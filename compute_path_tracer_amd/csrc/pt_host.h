@@ -20,10 +20,12 @@ struct PtJitModule {
     std::string key;  // generated source
 };
 
-// Source of the specialised kernel for these derived nodes (only the
-// topology, per-node flags and material indices enter; values stay in the
-// node table so value-only edits do not recompile).
-std::string pt_jit_source(const std::vector<PtNode> &nodes);
+// Source of the specialised kernel for these derived nodes.  bake=false:
+// only the topology, per-node flags and material indices enter (values stay
+// in the node table, value-only edits do not recompile); bake=true: node
+// values become exact f32 literals too (no scalar loads; recompiles, cached,
+// when a value changes).
+std::string pt_jit_source(const std::vector<PtNode> &nodes, bool bake);
 // Compile with hipRTC for gfx950; returns the code object or an error log.
 bool pt_jit_compile_source(const std::string &src, std::vector<char> &code, std::string &log);
 // Load a code object on the current device.

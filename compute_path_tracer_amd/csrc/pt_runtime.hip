@@ -62,6 +62,7 @@ struct pt_ctx {
     int kernel = -1;       // PT_KERNEL_*; -1 = environment / auto
     int shade_batch = -1;  // -1 = environment / default
     int jit = -1;          // 1 use per-scene hipRTC kernels, 0 interpreter; -1 = env (PT_JIT), default 1
+    int jit_bake = -1;     // 1 bake node values as literals; -1 = env (PT_JIT_BAKE), default 1
     PtJitModule jit_mod;   // loaded scene kernel (key = its source)
     std::string jit_log;
     double jit_seconds = 0.0;
@@ -80,6 +81,15 @@ std::mutex &jit_mutex() {
     return m;
 }
 
+bool jit_bake(const pt_ctx *c) {
+    if (c->jit_bake >= 0) return c->jit_bake != 0;
+    static const int env = [] {
+        const char *v = std::getenv("PT_JIT_BAKE");
+        return v ? std::atoi(v) : 1;
+    }();
+    return env != 0;
+}
+
 bool jit_wanted(const pt_ctx *c) {
     if (c->jit >= 0) return c->jit != 0;
     static const int env = [] {
@@ -96,7 +106,7 @@ void jit_refresh(pt_ctx *c, const std::vector<PtNode> &nodes) {
         pt_jit_unload(c->jit_mod);
         return;
     }
-    std::string src = pt_jit_source(nodes);
+    std::string src = pt_jit_source(nodes, jit_bake(c));
     if (c->jit_mod.module && c->jit_mod.key == src) return;
     pt_jit_unload(c->jit_mod);
     std::vector<char> code;
@@ -592,6 +602,11 @@ int pt_set_option(pt_ctx *c, const char *key, int value) {
         if (value != 0 && value != 1) return fail(c, PT_ERR_INVALID, "jit must be 0 or 1");
         c->jit = value;
         if (!value) pt_jit_unload(c->jit_mod);  // re-enabled on the next pt_set_data
+        return PT_OK;
+    }
+    if (!std::strcmp(key, "jit_bake")) {
+        if (value != 0 && value != 1) return fail(c, PT_ERR_INVALID, "jit_bake must be 0 or 1");
+        c->jit_bake = value;  // takes effect at the next pt_set_data
         return PT_OK;
     }
     if (!std::strcmp(key, "shade_batch")) {

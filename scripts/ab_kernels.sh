@@ -8,6 +8,6 @@ IFS=';' read -ra VARS <<< "${AB_VARIANTS:-PT_JIT=0 PT_SHADE_BATCH=8;PT_JIT=1 PT_
 for v in "${VARS[@]}"; do
   env $v timeout -k 10 300 python bench.py --steps ${AB_STEPS:-3} --warmup 1 --no-cpu-baseline ${AB_ARGS:-} > gpurun_out/ab.tmp 2>&1
   rc=$?
-  echo "$v rc=$rc $(python -c "import json,sys; d=json.loads(open('gpurun_out/ab.tmp').read().strip().splitlines()[-1]); print(d["value"], d["roofline"]["kernel_ms_per_launch"], d.get("schedule"))" 2>/dev/null)" | tee -a gpurun_out/ab.log
+  echo "$v rc=$rc $(python scripts/parse_bench.py gpurun_out/ab.tmp 2>/dev/null)" | tee -a gpurun_out/ab.log
   if [ $rc -ne 0 ]; then cat gpurun_out/ab.tmp; exit $rc; fi
 done
