@@ -62,7 +62,7 @@ struct pt_ctx {
     int kernel = -1;       // PT_KERNEL_*; -1 = environment / auto
     int shade_batch = -1;  // -1 = environment / default
     int jit = -1;          // 1 use per-scene hipRTC kernels, 0 interpreter; -1 = env (PT_JIT), default 1
-    int jit_bake = -1;     // 1 bake node values as literals; -1 = env (PT_JIT_BAKE), default 1
+    int jit_bake = -1;     // 1 bake node values as literals; -1 = env (PT_JIT_BAKE), default 0
     PtJitModule jit_mod;   // loaded scene kernel (key = its source)
     std::string jit_log;
     double jit_seconds = 0.0;
@@ -85,7 +85,7 @@ bool jit_bake(const pt_ctx *c) {
     if (c->jit_bake >= 0) return c->jit_bake != 0;
     static const int env = [] {
         const char *v = std::getenv("PT_JIT_BAKE");
-        return v ? std::atoi(v) : 1;
+        return v ? std::atoi(v) : 0;
     }();
     return env != 0;
 }
