@@ -124,11 +124,17 @@ def main() -> None:
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-row-stride", type=int, default=1)
     ap.add_argument("--cpu-spp", type=int, default=6)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo + host image reduce: rehearsal with ranks sharing one GPU")
+    ap.add_argument("--validate", action="store_true",
+                    help="rank 0 re-renders every frame on one GPU and checks the assembled image bit for bit")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("PT_BENCH_SHARE_GPU"):  # test aid: all ranks on GPU 0 (single-GPU boxes)
+        local_rank = 0
     dist = None
     if world > 1:
         import torch
@@ -136,7 +142,10 @@ def main() -> None:
 
         dist = dist_
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
 
     from compute_path_tracer_amd import _native as N
     from compute_path_tracer_amd import scenes
@@ -151,14 +160,17 @@ def main() -> None:
     pt = PathTracer(args.width, args.height, prog, device=local_rank, settings=settings)
     aspect = float(np.float32(args.width) / np.float32(args.height))
     spp_step = args.spp * world  # weak scaling: each rank owns 1/world of the tiles
-    tr = TileSplitRender(pt, rank, world, aspect)
+    tr = TileSplitRender(pt, rank, world, aspect, reduce="rccl" if args.dist_backend == "nccl" else "host")
 
     def barrier():
         if dist is not None:
             import torch
 
             torch.cuda.synchronize()
-            dist.barrier()
+            if args.dist_backend == "nccl":
+                dist.barrier(device_ids=[local_rank])
+            else:
+                dist.barrier()
 
     def step():
         tr.step(args.spp)
@@ -183,13 +195,23 @@ def main() -> None:
     if dist is not None:
         import torch
 
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     if world > 1:
         # per-launch kernel time on this rank (events on the library stream)
         tr.step(args.spp)
         kernel_ms.append(pt.last_dispatch_ms())
+    validation = None
+    if args.validate:
+        img = tr.image(0)  # every frame rendered so far, assembled on rank 0
+        if rank == 0:
+            ref = PathTracer(args.width, args.height, prog, device=local_rank, settings=settings)
+            ref.dispatch(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), tr.frame - 1)
+            want = ref.read_image()
+            validation = {"frames": tr.frame - 1,
+                          "bit_exact": bool(np.array_equal(img.view(np.uint32), want.view(np.uint32)))}
+            ref.close()
 
     pixels = args.width * args.height
     samples_step = pixels * args.spp * world  # all ranks
@@ -198,7 +220,7 @@ def main() -> None:
 
     if rank != 0:
         if dist is not None:
-            dist.barrier()
+            barrier()
             dist.destroy_process_group()
         return
 
@@ -237,6 +259,8 @@ def main() -> None:
         "schedule": schedule_metrics(st),
         "jit": {"active": bool(pt.get_option("jit_active")), "compile_s": round(pt.get_option("jit_seconds"), 3)},
     }
+    if validation is not None:
+        out["validation"] = validation
     tr_prof = profiled_traffic(out["config"])
     if tr_prof is not None:
         out["roofline"]["traffic"] = tr_prof[0]
@@ -247,7 +271,7 @@ def main() -> None:
                                            args.cpu_row_stride, args.cpu_spp)
     print(json.dumps(out), flush=True)
     if dist is not None:
-        dist.barrier()
+        barrier()
         dist.destroy_process_group()
 
 

@@ -46,14 +46,19 @@ class TileSplitRender:
     """
 
     def __init__(self, renderer, rank: int, world: int, aspect: float,
-                 broadcast: Optional[Callable] = None, frame0: int = 1):
+                 broadcast: Optional[Callable] = None, frame0: int = 1, reduce: str = "rccl"):
+        """reduce="rccl": pt_reduce_accum inside the library (RCCL over xGMI).
+        reduce="host": copy to host and sum with torch.distributed (gloo) --
+        a rehearsal aid for ranks that share one GPU, where RCCL refuses."""
         self.r = renderer
         self.rank, self.world = rank, world
         self.aspect = float(aspect)
         self.frame = frame0
         self.last_clear = frame0
+        self.mode = reduce
+        self._host = None
         renderer.set_tiles(rank, world)
-        if world > 1:
+        if world > 1 and reduce == "rccl":
             bcast = broadcast or torch_broadcast_object
             uid = bcast(renderer.comm_unique_id() if rank == 0 else None)
             renderer.comm_init(world, rank, uid)
@@ -70,12 +75,23 @@ class TileSplitRender:
         return n
 
     def reduce(self, root: int = 0) -> None:
-        if self.world > 1:
+        if self.world == 1:
+            return
+        if self.mode == "rccl":
             self.r.reduce(root)
+            return
+        import torch
+        import torch.distributed as dist
+
+        t = torch.from_numpy(self.r.read_image())
+        dist.reduce(t, dst=root, op=dist.ReduceOp.SUM)
+        self._host = t.numpy() if self.rank == root else None
 
     def image(self, root: int = 0) -> Optional[np.ndarray]:
         """The assembled image on ``root`` (None elsewhere)."""
         if self.world == 1:
             return self.r.read_image()
-        self.r.reduce(root)
-        return self.r.read_reduced() if self.rank == root else None
+        self.reduce(root)
+        if self.rank != root:
+            return None
+        return self.r.read_reduced() if self.mode == "rccl" else self._host

@@ -64,13 +64,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, mode):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     rows = scenes.c2_sphere_box_torus().rows()
     aspect = float(np.float32(W) / np.float32(H))
-    tr = TileSplitRender(OracleRenderer(rows, W, H), rank, world, aspect)
+    tr = TileSplitRender(OracleRenderer(rows, W, H), rank, world, aspect, reduce=mode)
     tr.step(SPP)  # SPP * world frames of this rank's tiles
     tr.step(SPP)
     img = tr.image(0)
@@ -80,10 +80,12 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_tile_split_reduce_matches_single_rank(tmp_path, world):
+@pytest.mark.parametrize("world,mode", [(2, "rccl"), (2, "host"), (3, "host")])
+def test_tile_split_reduce_matches_single_rank(tmp_path, world, mode):
+    """mode "rccl" drives the renderer's own reduce (RCCL in PathTracer, gloo
+    in the test double); "host" is TileSplitRender's torch.distributed sum."""
     out = str(tmp_path / "img.npy")
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, mode), nprocs=world, join=True)
     got = np.load(out, allow_pickle=False)
     rows = scenes.c2_sphere_box_torus().rows()
     aspect = float(np.float32(W) / np.float32(H))
