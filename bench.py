@@ -69,6 +69,10 @@ def schedule_metrics(st: dict) -> dict:
         out["idle_shade"] = round(st["idle_shade"] / (64.0 * st["wave_iters"]), 4)
         out["idle_free"] = round(st["idle_free"] / (64.0 * st["wave_iters"]), 4)
         out["maps_per_sample"] = round(maps / max(1, st["samples"]), 2)
+    if st.get("cyc_total"):  # share of wave time per phase (instrumented kernel)
+        out["wave_time"] = {k: round(st["cyc_" + k] / st["cyc_total"], 4)
+                            for k in ("refill", "bounds", "map", "shade")}
+        out["wave_cycles_per_iter"] = round(st["cyc_total"] / max(1, st["wave_iters"]), 1)
     return out
 
 
@@ -113,9 +117,10 @@ def cpu_baseline(scene, w, h, bounces, threads: int, row_stride: int, spp: int) 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=16)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--spp", type=int, default=16, help="frames per pixel per step (per GPU-share)")
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--spp", type=int, default=64,
+                    help="frames per pixel per step (per GPU-share); 4 steps x 64 = the 256-spp C3 config")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=8)

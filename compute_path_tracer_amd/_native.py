@@ -27,11 +27,14 @@ PT_OP_UNION_BEGIN, PT_OP_SHAPE, PT_OP_UNION_END = 0, 1, 2
 PT_COMBINE_ASSIGN, PT_COMBINE_UNION, PT_COMBINE_SUBTRACTION = 0, 1, 2
 PT_SO_SCALAR, PT_SO_VEC3, PT_SO_ONE, PT_SO_TORUS = 0, 1, 2, 3
 PT_COMM_ID_BYTES = 128
-PT_STAT_COUNT = 24
+PT_STAT_COUNT = 32
 STAT_NAMES = (
     "samples", "segments", "march_steps", "normal_maps", "shaded", "aabb_tests", "xform_union", "xform_shape",
     "sdf_sphere", "sdf_cube", "sdf_torus", "sdf_octahedron", "comb_union", "comb_sub", "comb_assign", "rr_break",
-    "wave_maps", "wave_shapes", "wave_iters", "lane_idle", "idle_shade", "idle_free", "reserved0", "reserved1",
+    "wave_maps", "wave_shapes", "wave_iters", "lane_idle", "idle_shade", "idle_free",
+    # wavefront kernel, wave-clock cycles (s_memtime) per phase, summed over waves
+    "cyc_refill", "cyc_bounds", "cyc_map", "cyc_shade", "cyc_total",
+    "reserved27", "reserved28", "reserved29", "reserved30", "reserved31",
 )
 
 SYMBOLS = (

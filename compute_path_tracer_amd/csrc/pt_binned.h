@@ -1,0 +1,419 @@
+// pt_binned.h -- the mask-binned wavefront schedule (PT_KERNEL_BINNED).
+//
+// Same per-sample arithmetic as the reference loop (pt_path.h), different
+// grouping of work.  The tile-resident wavefront kernel (pt_wave.h) keeps a
+// lane's path on that lane, so after the first bounce the 64 lanes of a wave
+// march rays whose check[] sets (bounds(), test_compute.glsl:101) differ and
+// the wave pays for the union of their shapes.  Here every bounce is one pass
+// over all live paths of a chunk of frames:
+//
+//   gen     camera rays of every (pixel, frame) + their bounds() mask
+//   bin     histogram of mask bins -> prefix sum -> scatter, which moves the
+//           rays (64 B) and masks into bin order
+//   trace   persistent waves take runs of the binned rays, 64 at a time into
+//           staging registers (one window prefetched ahead), and march,
+//           calc_normal and shade them; ended paths store their colour, the
+//           others write their next ray back at the same position
+//   bounds  bounds() mask + bin of every written-back ray (next pass)
+//   fold    each pixel mixes its frames' colours in frame order
+//
+// Paths are independent and the fold runs in frame order, so the schedule
+// changes nothing in the image: it is bit-identical to the other kernels.
+#pragma once
+
+#include "pt_path.h"
+
+#define PT_BIN_BITS 12
+#define PT_BINS (1 << PT_BIN_BITS)
+#define PT_BIN_NONE 0xffffffffu
+#define PT_BIN_BLOCK 256  // threads per block of the gen / bounds / scatter kernels
+#define PT_SCATTER_ITEMS 16
+
+struct PtRay {  // a path between two segments, 64 B
+    float ro[3];
+    float rd[3];
+    float thr[3];
+    float ret[3];
+    uint32_t rng;
+    uint32_t sid;  // sample slot: frame * n_pix + local pixel; PT_BIN_NONE: path ended
+    uint32_t pad[2];
+};
+
+struct PtPass {
+    PtLaunch L;             // scene tables, image, frame0 / last_clear0 of this chunk
+    PtRay *ru;              // unbinned rays: gen's camera rays, trace's written-back next rays
+    PtRay *rs;              // the same rays in bin order (scatter -> trace)
+    uint4 *mask_u;          // check[] bits per ru slot (gen / bounds)
+    uint4 *mask_s;          // ... in bin order
+    uint32_t *key;          // bin per ru slot (PT_BIN_NONE: no live ray)
+    uint32_t *hist;         // [PT_BINS] counts, zero outside gen/bounds -> scan
+    uint32_t *offs;         // [PT_BINS] scatter cursors
+    uint32_t *ctrl;         // this pass: [0] binned rays, [1] trace run cursor
+    const uint32_t *n_src;  // ru slots (bounds / scatter), null: n_src_const
+    float4 *color;          // [frames][n_pix] sample colours
+    uint32_t n_src_const;
+    int32_t bounce;         // segment index of this pass (path_trace's loop counter i)
+    int32_t n_pix;          // local pixel slots: n_tiles * 64
+    int32_t frames;         // frames in this chunk
+};
+
+namespace pt {
+
+__device__ __forceinline__ uint32_t bin_of(const uint4 &m) {
+    if ((m.y | m.z | m.w) == 0u && m.x < uint32_t(PT_BINS)) return m.x;  // small scenes: the exact set
+    const uint32_t h = (m.x * 0x9E3779B1u) ^ (m.y * 0x85EBCA77u) ^ (m.z * 0xC2B2AE3Du) ^ (m.w * 0x27D4EB2Fu);
+    return (h ^ (h >> 15)) * 0x2C1B3C6Du >> (32 - PT_BIN_BITS);
+}
+
+// bounds() of one ray, one thread: every box's slab test (scalar box loads).
+template <bool ST>
+__device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro, const pt_f3 &rd, Stats<ST> &st) {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    const caabb_ptr boxes = (caabb_ptr)L.aabbs;
+    for (int b = 0; b < L.n_aabb; ++b) {
+        const PtAabb bx = boxes[b];
+        if (ray_box(bx, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z)) w[bx.back >> 5] |= 1u << (bx.back & 31);
+    }
+    st.add(PT_ST_SEGMENTS);
+    st.add(PT_ST_AABB, uint32_t(L.n_aabb));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void store_ray(PtRay *r, const pt_f3 &ro, const pt_f3 &rd, const pt_f3 &thr,
+                                          const pt_f3 &ret, uint32_t rng, uint32_t sid) {
+    float4 *v = reinterpret_cast<float4 *>(r);
+    v[0] = make_float4(ro.x, ro.y, ro.z, rd.x);
+    v[1] = make_float4(rd.y, rd.z, thr.x, thr.y);
+    v[2] = make_float4(thr.z, ret.x, ret.y, ret.z);
+    reinterpret_cast<uint4 *>(r)[3] = make_uint4(rng, sid, 0u, 0u);
+}
+
+__device__ __forceinline__ void load_ray(const PtRay *r, pt_f3 &ro, pt_f3 &rd, pt_f3 &thr, pt_f3 &ret, uint32_t &rng,
+                                         uint32_t &sid) {
+    const float4 *v = reinterpret_cast<const float4 *>(r);
+    const float4 a = v[0], b = v[1], c = v[2];
+    const uint4 d = reinterpret_cast<const uint4 *>(r)[3];
+    ro = pt_f3{a.x, a.y, a.z};
+    rd = pt_f3{a.w, b.x, b.y};
+    thr = pt_f3{b.z, b.w, c.x};
+    ret = pt_f3{c.y, c.z, c.w};
+    rng = d.x;
+    sid = d.y;
+}
+
+__device__ __forceinline__ void hist_zero(uint32_t *lh) {
+    for (int b = int(threadIdx.x); b < PT_BINS; b += int(blockDim.x)) lh[b] = 0u;
+    __syncthreads();
+}
+__device__ __forceinline__ void hist_flush(const uint32_t *lh, uint32_t *hist) {
+    __syncthreads();
+    for (int b = int(threadIdx.x); b < PT_BINS; b += int(blockDim.x))
+        if (lh[b] != 0u) atomicAdd(&hist[b], lh[b]);
+}
+
+// local pixel slot -> image coordinates (cyclic tile ownership, as pt_wave.h)
+__device__ __forceinline__ void pixel_of(const PtLaunch &L, uint32_t pl, int &x, int &y) {
+    const int k = int(pl >> 6), p = int(pl & 63u);
+    const int g = L.rank + k * L.nranks;
+    x = (g % L.tiles_x) * PT_TILE + (p & 7);
+    y = (g / L.tiles_x) * PT_TILE + (p >> 3);
+}
+
+// gen: camera ray + bounds() of every (frame, pixel) of the chunk.
+template <bool ST>
+__device__ __forceinline__ void bin_gen_body(const PtPass &P) {
+    __shared__ uint32_t lh[PT_BINS];
+    hist_zero(lh);
+    Stats<ST> st;
+    st.init();
+    const PtLaunch &L = P.L;
+    const uint32_t npix = uint32_t(P.n_pix), n = npix * uint32_t(P.frames);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t f = i / npix, pl = i - f * npix;
+        int x, y;
+        pixel_of(L, pl, x, y);
+        if (x >= L.width || y >= L.height) {
+            P.key[i] = PT_BIN_NONE;
+            continue;
+        }
+        uint32_t rng;
+        pt_f3 ro, rd;
+        camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), L.width, L.height, L.aspect, L.fov, rng, ro, rd);
+        st.add(PT_ST_SAMPLES);
+        store_ray(P.ru + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, pt_f3{0.0f, 0.0f, 0.0f}, rng, i);
+        const uint4 m = bounds_mask<ST>(L, ro, rd, st);
+        P.mask_u[i] = m;
+        const uint32_t b = bin_of(m);
+        P.key[i] = b;
+        atomicAdd(&lh[b], 1u);
+    }
+    hist_flush(lh, P.hist);
+    flush_stats<ST>(L, st);
+}
+
+// bounds: mask + bin of every ray the last trace pass wrote back.
+template <bool ST>
+__device__ __forceinline__ void bin_bounds_body(const PtPass &P) {
+    __shared__ uint32_t lh[PT_BINS];
+    hist_zero(lh);
+    Stats<ST> st;
+    st.init();
+    const PtLaunch &L = P.L;
+    const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 *v = reinterpret_cast<const float4 *>(P.ru + i);
+        if (reinterpret_cast<const uint4 *>(v)[3].y == PT_BIN_NONE) {  // path ended in the last pass
+            P.key[i] = PT_BIN_NONE;
+            continue;
+        }
+        const float4 a = v[0], b = v[1];
+        const uint4 m = bounds_mask<ST>(L, pt_f3{a.x, a.y, a.z}, pt_f3{a.w, b.x, b.y}, st);
+        P.mask_u[i] = m;
+        const uint32_t k = bin_of(m);
+        P.key[i] = k;
+        atomicAdd(&lh[k], 1u);
+    }
+    hist_flush(lh, P.hist);
+    flush_stats<ST>(L, st);
+}
+
+// scan: exclusive prefix of the histogram (one block of PT_BINS/4 threads);
+// clears the histogram and this pass's cursors.
+__device__ __forceinline__ void bin_scan_body(const PtPass &P) {
+    __shared__ uint32_t part[PT_BINS / 4];
+    const int t = int(threadIdx.x);
+    uint32_t v[4], sum = 0u;
+    for (int j = 0; j < 4; ++j) {
+        v[j] = P.hist[t * 4 + j];
+        sum += v[j];
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < PT_BINS / 4; off <<= 1) {
+        const uint32_t x = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    for (int j = 0; j < 4; ++j) {
+        P.offs[t * 4 + j] = run;
+        run += v[j];
+        P.hist[t * 4 + j] = 0u;
+    }
+    if (t == PT_BINS / 4 - 1) {
+        P.ctrl[0] = part[t];
+        P.ctrl[1] = 0u;
+    }
+}
+
+// scatter: live rays and their masks into bin order.  Per block tile, the
+// rays of one bin take consecutive places (LDS ranks) after one global
+// reservation.
+__device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
+    __shared__ uint32_t cnt[PT_BINS];
+    const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
+    const uint32_t tile = PT_BIN_BLOCK * PT_SCATTER_ITEMS;
+    for (uint32_t t0 = blockIdx.x * tile; t0 < n; t0 += gridDim.x * tile) {
+        hist_zero(cnt);
+        uint32_t kk[PT_SCATTER_ITEMS], rr[PT_SCATTER_ITEMS];
+#pragma unroll
+        for (int j = 0; j < PT_SCATTER_ITEMS; ++j) {
+            const uint32_t e = t0 + uint32_t(j * PT_BIN_BLOCK) + threadIdx.x;
+            kk[j] = e < n ? P.key[e] : PT_BIN_NONE;
+            rr[j] = kk[j] != PT_BIN_NONE ? atomicAdd(&cnt[kk[j]], 1u) : 0u;
+        }
+        __syncthreads();
+        for (int b = int(threadIdx.x); b < PT_BINS; b += PT_BIN_BLOCK) {
+            const uint32_t c = cnt[b];
+            if (c != 0u) cnt[b] = atomicAdd(&P.offs[b], c);
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int j = 0; j < PT_SCATTER_ITEMS; ++j)
+            if (kk[j] != PT_BIN_NONE) {
+                const uint32_t src = t0 + uint32_t(j * PT_BIN_BLOCK) + threadIdx.x, dst = cnt[kk[j]] + rr[j];
+                const uint4 *a = reinterpret_cast<const uint4 *>(P.ru + src);
+                uint4 *b = reinterpret_cast<uint4 *>(P.rs + dst);
+                const uint4 v0 = a[0], v1 = a[1], v2 = a[2], v3 = a[3], m = P.mask_u[src];
+                b[0] = v0;
+                b[1] = v1;
+                b[2] = v2;
+                b[3] = v3;
+                P.mask_s[dst] = m;
+            }
+        __syncthreads();
+    }
+}
+
+// trace: one wave per block, persistent.  The wave takes runs of the binned
+// rays (so its lanes share their check[] set); within a run, windows of 64
+// rays are loaded into staging registers one window ahead and handed to free
+// lanes by cross-lane moves.  Lanes run the MARCH -> NORMAL -> SHADE state
+// machine of pt_path.h; a shaded path either ends (colour stored) or writes
+// its next ray back to ru at its binned position.
+template <class Map, bool ST>
+__device__ __forceinline__ void bin_trace_body(const PtPass &P) {
+    const PtLaunch &L = P.L;
+    const int lane = int(threadIdx.x);
+    Stats<ST> st;
+    st.init();
+    const uint64_t t_start = st.clk();
+    const uint32_t n = P.ctrl[0];
+    // run length: about 8 runs per wave, 64..1024 rays, whole windows
+    uint32_t R = n / (gridDim.x * 8u);
+    R = R < 64u ? 64u : (R > 1024u ? 1024u : (R + 63u) & ~63u);
+    const int shade_batch = L.shade_batch > 0 ? L.shade_batch : 1;
+
+    // runs [run_cur, run_end); the next run is reserved one run ahead
+    uint32_t nxt = 0u;
+    if (lane == 0) nxt = atomicAdd(&P.ctrl[1], R);
+    uint32_t run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt))), run_end = 0u;
+    run_end = run_cur < n ? (run_cur + R < n ? run_cur + R : n) : run_cur;
+    if (lane == 0 && run_cur < n) nxt = atomicAdd(&P.ctrl[1], R);
+    // staging window: lane j holds the ray at binned position wbase + j
+    uint32_t wbase = run_cur, wcnt = 0u, wtake = 0u;
+    float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0, s2 = s0;
+    uint4 s3 = make_uint4(0u, 0u, 0u, 0u), sm = s3;
+    auto load_window = [&]() {
+        if (run_cur >= run_end) {  // next run
+            run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt)));
+            run_end = run_cur < n ? (run_cur + R < n ? run_cur + R : n) : run_cur;
+            if (lane == 0 && run_cur < n) nxt = atomicAdd(&P.ctrl[1], R);
+        }
+        wbase = run_cur;
+        wcnt = run_end - run_cur < 64u ? run_end - run_cur : 64u;
+        wtake = 0u;
+        run_cur += wcnt;
+        if (uint32_t(lane) < wcnt) {
+            const uint4 *v = reinterpret_cast<const uint4 *>(P.rs + wbase + uint32_t(lane));
+            const uint4 a = v[0], b = v[1], c = v[2];
+            s0 = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+            s1 = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w));
+            s2 = make_float4(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w));
+            s3 = v[3];
+            sm = P.mask_s[wbase + uint32_t(lane)];
+        }
+    };
+    load_window();
+
+    int state = ST_FREE;
+    uint32_t rng = 0u, sid = 0u, pos = 0u;
+    pt_f3 ro{0.0f, 0.0f, 0.0f}, rd{0.0f, 0.0f, 1.0f};
+    pt_f3 thr{1.0f, 1.0f, 1.0f}, ret{0.0f, 0.0f, 0.0f};
+    int seg = 0, step = 0, mat = 0;
+    float t = 0.0f;
+    float dv0 = 0.0f, dv1 = 0.0f, dv2 = 0.0f;
+    Check ck{0ull, 0ull};
+
+    for (;;) {
+        uint64_t tm = st.clk();
+        // ---- 1. refill free lanes from the staging window --------------
+        const uint64_t freem = __ballot(state == ST_FREE);
+        if (freem != 0ull && wcnt != 0u) {
+            const uint32_t avail = wcnt - wtake, nf = uint32_t(__popcll(freem));
+            const uint32_t take = nf < avail ? nf : avail;
+            const int r = lane_rank(freem);
+            const int src = int(wtake) + r;
+            const bool got = state == ST_FREE && uint32_t(r) < take;
+            // cross-lane moves of the staged ray (every lane takes part)
+            const float a0 = __shfl(s0.x, src, 64), a1 = __shfl(s0.y, src, 64), a2 = __shfl(s0.z, src, 64),
+                        a3 = __shfl(s0.w, src, 64);
+            const float b0 = __shfl(s1.x, src, 64), b1 = __shfl(s1.y, src, 64), b2 = __shfl(s1.z, src, 64),
+                        b3 = __shfl(s1.w, src, 64);
+            const float c0 = __shfl(s2.x, src, 64), c1 = __shfl(s2.y, src, 64), c2 = __shfl(s2.z, src, 64),
+                        c3 = __shfl(s2.w, src, 64);
+            const uint32_t d0 = uint32_t(__shfl(int(s3.x), src, 64)), d1 = uint32_t(__shfl(int(s3.y), src, 64));
+            const uint32_t m0 = uint32_t(__shfl(int(sm.x), src, 64)), m1 = uint32_t(__shfl(int(sm.y), src, 64)),
+                           m2 = uint32_t(__shfl(int(sm.z), src, 64)), m3 = uint32_t(__shfl(int(sm.w), src, 64));
+            if (got) {
+                ro = pt_f3{a0, a1, a2};
+                rd = pt_f3{a3, b0, b1};
+                thr = pt_f3{b2, b3, c0};
+                ret = pt_f3{c1, c2, c3};
+                rng = d0;
+                sid = d1;
+                ck.lo = uint64_t(m0) | (uint64_t(m1) << 32);
+                ck.hi = uint64_t(m2) | (uint64_t(m3) << 32);
+                pos = wbase + uint32_t(src);
+                seg = P.bounce;
+                t = 0.0f;
+                step = 0;
+                state = ST_MARCH;
+            }
+            wtake += take;
+            if (wtake == wcnt) load_window();  // wcnt = 0: no rays left for this wave
+        }
+        const bool more = wcnt != 0u;
+        tm = st.lap(PT_ST_CYC_REFILL, tm);
+
+        // ---- 2. one map() per marching / normal-tap lane ------------------
+        const bool mapping = state == ST_MARCH || state == ST_NORMAL;
+        st.add(PT_ST_LANE_IDLE, mapping ? 0u : 1u);
+        st.add(PT_ST_IDLE_SHADE, state == ST_SHADE ? 1u : 0u);
+        st.add(PT_ST_IDLE_FREE, state == ST_FREE ? 1u : 0u);
+        if (lane == 0) st.add(PT_ST_WAVE_ITERS);
+        if (__ballot(mapping) != 0ull) {
+            if (lane == 0) st.add(PT_ST_WAVE_MAPS);
+            if (mapping) {
+                float qx, qy, qz;
+                map_point(state, step, ro, rd, t, qx, qy, qz);
+                const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, st);
+                after_map<ST>(h, state, step, t, ro, rd, mat, dv0, dv1, dv2, st);
+            }
+        }
+        tm = st.lap(PT_ST_CYC_MAP, tm);
+
+        // ---- 3. shading (batched); ended paths store, the rest write back --
+        const uint64_t shadem = __ballot(state == ST_SHADE);
+        if (shadem != 0ull &&
+            (__popcll(shadem) >= shade_batch || __ballot(state == ST_MARCH || state == ST_NORMAL) == 0ull || !more)) {
+            if (state == ST_SHADE) {
+                const bool done =
+                    shade_lane<ST>(L.mats, L.bounces, mat, dv0, dv1, dv2, step, rng, ro, rd, thr, ret, seg, st);
+                if (done) {
+                    const pt_f3 c = final_color(L.debug, seg, L.bounces, ret);
+                    P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
+                    reinterpret_cast<uint4 *>(P.ru + pos)[3] = make_uint4(rng, PT_BIN_NONE, 0u, 0u);
+                } else {
+                    store_ray(P.ru + pos, ro, rd, thr, ret, rng, sid);
+                }
+                state = ST_FREE;
+            }
+        }
+        tm = st.lap(PT_ST_CYC_SHADE, tm);
+        if (!more && __ballot(state != ST_FREE) == 0ull) break;
+    }
+    (void)st.lap(PT_ST_CYC_TOTAL, t_start);
+    flush_stats<ST>(L, st);
+}
+
+// fold: every pixel mixes its frames in order (test_compute.glsl:240-245).
+__device__ __forceinline__ void bin_fold_body(const PtPass &P) {
+    const PtLaunch &L = P.L;
+    const uint32_t pl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pl >= uint32_t(P.n_pix) || !L.write) return;
+    int x, y;
+    pixel_of(L, pl, x, y);
+    if (x >= L.width || y >= L.height) return;
+    float4 *texel = reinterpret_cast<float4 *>(L.accum + (size_t(y) * size_t(L.width) + size_t(x)) * 4);
+    const size_t stride = size_t(P.n_pix);
+    if (L.debug != 0) {  // direct store of the chunk's (single) frame
+        const float4 c = P.color[size_t(P.frames - 1) * stride + pl];
+        *texel = make_float4(c.x, c.y, c.z, 1.0f);
+        return;
+    }
+    const float4 v = *texel;
+    float ar = v.x, ag = v.y, ab = v.z;
+    for (int f = 0; f < P.frames; ++f) {
+        const float4 c = P.color[size_t(f) * stride + pl];
+        const int32_t lc = int32_t(uint32_t(L.last_clear0) + uint32_t(f));
+        const float w = 1.0f / float(lc + 1), omw = 1.0f - w;
+        ar = ar * omw + c.x * w;
+        ag = ag * omw + c.y * w;
+        ab = ab * omw + c.z * w;
+    }
+    *texel = make_float4(ar, ag, ab, 1.0f);
+}
+
+}  // namespace pt

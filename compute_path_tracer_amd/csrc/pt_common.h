@@ -50,6 +50,20 @@ struct Stats {
     __device__ __forceinline__ void add(int k, uint32_t v = 1) {
         if constexpr (ST) c[k] += v;
     }
+    // wave clock for the per-phase cycle counters (instrumented kernel only)
+    __device__ __forceinline__ uint64_t clk() const {
+        if constexpr (ST) return __builtin_readcyclecounter();
+        return 0;
+    }
+    // charge the cycles since `t` to slot k (lane 0 only), return the new mark
+    __device__ __forceinline__ uint64_t lap(int k, uint64_t t) {
+        if constexpr (ST) {
+            const uint64_t now = __builtin_readcyclecounter();
+            if ((threadIdx.x & 63) == 0) c[k] += uint32_t(now - t);
+            return now;
+        }
+        return 0;
+    }
 };
 
 __device__ __forceinline__ int lane_rank(uint64_t m) {  // set bits of m below this lane

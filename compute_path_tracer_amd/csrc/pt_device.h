@@ -89,6 +89,11 @@ enum {
     PT_ST_LANE_IDLE,    // lanes without map work in an iteration (wavefront kernel)
     PT_ST_IDLE_SHADE,   //   ... of which waiting for a shading pass
     PT_ST_IDLE_FREE,    //   ... of which without a job (pool drained / ring full)
+    PT_ST_CYC_REFILL,   // wave clock cycles (s_memtime) spent per phase: job refill + camera rays
+    PT_ST_CYC_BOUNDS,   //   bounds() redistribution
+    PT_ST_CYC_MAP,      //   map() + state update
+    PT_ST_CYC_SHADE,    //   shading + fold
+    PT_ST_CYC_TOTAL,    //   whole wave
     PT_ST_COUNT
 };
 
@@ -121,6 +126,7 @@ struct PtLaunch {
 #define PT_KERNEL_AUTO 0
 #define PT_KERNEL_SIMPLE 1     // one path per lane, reference loop structure
 #define PT_KERNEL_WAVEFRONT 2  // per-lane state machine with job refill
+#define PT_KERNEL_BINNED 3     // per-bounce passes over mask-binned rays (pt_binned.h)
 #ifndef PT_RING
 #define PT_RING 4              // wavefront kernel: in-flight samples per pixel (power of 2)
 #endif

@@ -6,7 +6,15 @@
 #include <string>
 #include <vector>
 
+#include "pt_binned.h"
 #include "pt_device.h"
+
+// ahead-of-time kernels (pt_kernel.hip)
+bool pt_use_simple_kernel(const PtLaunch &L);
+void pt_launch_render(const PtLaunch &L, bool stats, hipStream_t stream);
+enum class PtBinStage { Gen, Bounds, Scan, Scatter, Trace, Fold };
+void pt_launch_bin(PtBinStage stage, const PtPass &P, bool stats, unsigned grid, hipStream_t stream);
+int pt_bin_trace_blocks_per_cu(bool stats);  // occupancy of the interpreter trace kernel
 
 // Expand (program, data[]) into the device tables (see pt_device.h).
 int pt_derive(const std::vector<pt_op> &ops, const std::vector<pt_aabb> &aabbs, const float *data, uint32_t n,
@@ -17,6 +25,8 @@ struct PtJitModule {
     hipModule_t module = nullptr;
     hipFunction_t render = nullptr;
     hipFunction_t render_stats = nullptr;
+    hipFunction_t trace = nullptr;        // binned pipeline trace pass (pt_binned.h)
+    hipFunction_t trace_stats = nullptr;
     std::string key;  // generated source
 };
 

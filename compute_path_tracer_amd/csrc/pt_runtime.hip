@@ -23,8 +23,6 @@
 #include "pt_host.h"
 #include "pt_math.h"
 
-void pt_launch_render(const PtLaunch &L, bool stats, hipStream_t stream);
-bool pt_use_simple_kernel(const PtLaunch &L);
 
 static_assert(sizeof(pt_constants) == 16, "Constants is 16 B (path_tracer.rs:149-155)");
 static_assert(sizeof(pt_settings) == 20, "Settings is 20 B (path_tracer.rs:157-163)");
@@ -63,7 +61,15 @@ struct pt_ctx {
     int shade_batch = -1;  // -1 = environment / default
     int jit = -1;          // 1 use per-scene hipRTC kernels, 0 interpreter; -1 = env (PT_JIT), default 1
     int jit_bake = -1;     // 1 bake node values as literals; -1 = env (PT_JIT_BAKE), default 0
+    int bin_samples = -1;  // binned pipeline: samples per chunk; -1 = env (PT_BIN_SAMPLES), default 2^25
     PtJitModule jit_mod;   // loaded scene kernel (key = its source)
+    // binned pipeline buffers (pt_binned.h), for bin_cap samples per chunk
+    PtRay *d_ray[2] = {nullptr, nullptr};  // unbinned, binned
+    uint4 *d_mask[2] = {nullptr, nullptr};
+    uint32_t *d_key = nullptr, *d_hist = nullptr, *d_offs = nullptr, *d_ctrl = nullptr;
+    float4 *d_color = nullptr;
+    size_t bin_cap = 0, ctrl_words = 0;
+    int cu_count = 0;
     std::string jit_log;
     double jit_seconds = 0.0;
     std::string err;
@@ -403,9 +409,148 @@ int pt_set_tiles(pt_ctx *c, uint32_t rank, uint32_t nranks) {
     return pt_resize_clear(c, c->width, c->height);
 }
 
+// ---- binned pipeline (pt_binned.h) -------------------------------------------
+// per sample of a chunk: rays and masks unbinned + binned, bin key, colour
+constexpr size_t kBinBytesPerSample = 2 * sizeof(PtRay) + 2 * sizeof(uint4) + sizeof(uint32_t) + sizeof(float4);
+
+static size_t bin_samples(const pt_ctx *c) {
+    if (c->bin_samples > 0) return size_t(c->bin_samples);
+    static const long env = [] {
+        const char *v = std::getenv("PT_BIN_SAMPLES");
+        return v ? std::atol(v) : 0L;
+    }();
+    return env >= 64 ? size_t(env) : (size_t(1) << 25);
+}
+
+static void free_bin(pt_ctx *c) {
+    (void)hipFree(c->d_ray[0]);
+    (void)hipFree(c->d_ray[1]);
+    (void)hipFree(c->d_mask[0]);
+    (void)hipFree(c->d_mask[1]);
+    (void)hipFree(c->d_key);
+    (void)hipFree(c->d_hist);
+    (void)hipFree(c->d_offs);
+    (void)hipFree(c->d_ctrl);
+    (void)hipFree(c->d_color);
+    c->d_ray[0] = c->d_ray[1] = nullptr;
+    c->d_mask[0] = c->d_mask[1] = nullptr;
+    c->d_key = c->d_hist = c->d_offs = c->d_ctrl = nullptr;
+    c->d_color = nullptr;
+    c->bin_cap = c->ctrl_words = 0;
+}
+
+static int ensure_bin(pt_ctx *c, size_t samples, size_t passes) {
+    const size_t words = 4 * (passes + 1);
+    if (samples <= c->bin_cap && words <= c->ctrl_words) return PT_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    samples = std::max(samples, c->bin_cap);
+    free_bin(c);
+    if (hipMalloc(&c->d_ray[0], samples * sizeof(PtRay)) != hipSuccess ||
+        hipMalloc(&c->d_ray[1], samples * sizeof(PtRay)) != hipSuccess ||
+        hipMalloc(&c->d_mask[0], samples * sizeof(uint4)) != hipSuccess ||
+        hipMalloc(&c->d_mask[1], samples * sizeof(uint4)) != hipSuccess ||
+        hipMalloc(&c->d_key, samples * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_color, samples * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->d_hist, PT_BINS * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_offs, PT_BINS * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_ctrl, words * sizeof(uint32_t)) != hipSuccess) {
+        free_bin(c);
+        (void)hipGetLastError();
+        return fail(c, PT_ERR_HIP, "out of device memory for the binned pipeline");
+    }
+    HIPCHK(c, hipMemset(c->d_hist, 0, PT_BINS * sizeof(uint32_t)));
+    c->bin_cap = samples;
+    c->ctrl_words = words;
+    if (!c->cu_count) HIPCHK(c, hipDeviceGetAttribute(&c->cu_count, hipDeviceAttributeMultiprocessorCount, c->device));
+    return PT_OK;
+}
+
+// One dispatch chunk through the pass pipeline: frames are processed in
+// sub-chunks of at most bin_samples() samples.
+static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
+    const uint32_t n_pix = uint32_t(L.n_tiles) * 64u;
+    int32_t frame0 = L.frame0, lc0 = L.last_clear0;
+    uint32_t spp = uint32_t(L.spp);
+    if (L.debug != 0) {  // direct stores: only the last frame survives (as the other kernels)
+        frame0 = int32_t(uint32_t(frame0) + spp - 1);
+        lc0 = int32_t(uint32_t(lc0) + spp - 1);
+        spp = 1;
+    }
+    const uint32_t F = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, bin_samples(c) / n_pix)));
+    const int passes = L.bounces + 1;
+    int rc = ensure_bin(c, size_t(n_pix) * F, size_t(passes));
+    if (rc != PT_OK) return rc;
+    const unsigned cu = unsigned(std::max(1, c->cu_count));
+    auto item_grid = [&](size_t n) {
+        return unsigned(std::max<size_t>(1, std::min<size_t>((n + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK, 4 * cu)));
+    };
+    auto scatter_grid = [&](size_t n) {
+        const size_t tile = PT_BIN_BLOCK * PT_SCATTER_ITEMS;
+        return unsigned(std::max<size_t>(1, std::min<size_t>((n + tile - 1) / tile, 4 * cu)));
+    };
+    const bool jit = c->jit_mod.module != nullptr;
+    hipFunction_t jf = jit ? (stats ? c->jit_mod.trace_stats : c->jit_mod.trace) : nullptr;
+    int per_cu = 0;
+    if (jit) HIPCHK(c, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jf, 64, 0));
+    else per_cu = pt_bin_trace_blocks_per_cu(stats);
+    const unsigned trace_grid = cu * unsigned(std::max(1, per_cu));
+
+    for (uint32_t done = 0; done < spp; done += F) {
+        const uint32_t fr = std::min(F, spp - done);
+        const size_t n0 = size_t(n_pix) * fr;
+        PtPass P;
+        std::memset(&P, 0, sizeof P);
+        P.L = L;
+        P.L.frame0 = int32_t(uint32_t(frame0) + done);
+        P.L.last_clear0 = int32_t(uint32_t(lc0) + done);
+        P.L.spp = int32_t(fr);
+        P.ru = c->d_ray[0];
+        P.rs = c->d_ray[1];
+        P.mask_u = c->d_mask[0];
+        P.mask_s = c->d_mask[1];
+        P.key = c->d_key;
+        P.hist = c->d_hist;
+        P.offs = c->d_offs;
+        P.color = c->d_color;
+        P.ctrl = c->d_ctrl;
+        P.n_src = nullptr;
+        P.n_src_const = uint32_t(n0);
+        P.n_pix = int32_t(n_pix);
+        P.frames = int32_t(fr);
+        pt_launch_bin(PtBinStage::Gen, P, stats, item_grid(n0), c->stream);
+        HIPCHK(c, hipGetLastError());
+        for (int k = 0; k < passes; ++k) {
+            // pass k: bin the rays in ru (gen's, or those trace k-1 wrote back), trace them
+            P.bounce = k;
+            P.ctrl = c->d_ctrl + 4 * k;
+            P.n_src = k == 0 ? nullptr : c->d_ctrl + 4 * (k - 1);
+            if (k > 0) {
+                pt_launch_bin(PtBinStage::Bounds, P, stats, item_grid(c->bin_cap), c->stream);
+                HIPCHK(c, hipGetLastError());
+            }
+            pt_launch_bin(PtBinStage::Scan, P, stats, 1, c->stream);
+            pt_launch_bin(PtBinStage::Scatter, P, stats, scatter_grid(k == 0 ? n0 : c->bin_cap), c->stream);
+            HIPCHK(c, hipGetLastError());
+            if (jit) {
+                void *args[] = {&P};
+                HIPCHK(c, hipModuleLaunchKernel(jf, trace_grid, 1, 1, 64, 1, 1, 0, c->stream, args, nullptr));
+            } else {
+                pt_launch_bin(PtBinStage::Trace, P, stats, trace_grid, c->stream);
+                HIPCHK(c, hipGetLastError());
+            }
+        }
+        pt_launch_bin(PtBinStage::Fold, P, stats, unsigned((n_pix + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK), c->stream);
+        HIPCHK(c, hipGetLastError());
+    }
+    return PT_OK;
+}
+
+static bool use_binned(const PtLaunch &L) { return L.kernel == PT_KERNEL_BINNED && !pt_use_simple_kernel(L); }
+
 // Launch one chunk: the scene-specialised wavefront kernel when loaded, else
 // the ahead-of-time kernels (pt_kernel.hip).
 static int launch(pt_ctx *c, PtLaunch &L, bool stats) {
+    if (use_binned(L)) return launch_binned(c, L, stats);
     if (!pt_use_simple_kernel(L) && c->jit_mod.module) {
         void *args[] = {&L};
         HIPCHK(c, hipModuleLaunchKernel(stats ? c->jit_mod.render_stats : c->jit_mod.render, unsigned(L.n_tiles), 1, 1,
@@ -450,6 +595,7 @@ static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, u
         if (!v) return PT_KERNEL_AUTO;
         if (!std::strcmp(v, "simple")) return PT_KERNEL_SIMPLE;
         if (!std::strcmp(v, "wave")) return PT_KERNEL_WAVEFRONT;
+        if (!std::strcmp(v, "binned")) return PT_KERNEL_BINNED;
         return PT_KERNEL_AUTO;
     }();
     static const int env_batch = [] {
@@ -594,7 +740,7 @@ int pt_last_dispatch_ms(pt_ctx *c, float *ms) {
 int pt_set_option(pt_ctx *c, const char *key, int value) {
     if (!c || !key) return PT_ERR_INVALID;
     if (!std::strcmp(key, "kernel")) {
-        if (value < PT_KERNEL_AUTO || value > PT_KERNEL_WAVEFRONT) return fail(c, PT_ERR_INVALID, "bad kernel id");
+        if (value < PT_KERNEL_AUTO || value > PT_KERNEL_BINNED) return fail(c, PT_ERR_INVALID, "bad kernel id");
         c->kernel = value;
         return PT_OK;
     }
@@ -607,6 +753,11 @@ int pt_set_option(pt_ctx *c, const char *key, int value) {
     if (!std::strcmp(key, "jit_bake")) {
         if (value != 0 && value != 1) return fail(c, PT_ERR_INVALID, "jit_bake must be 0 or 1");
         c->jit_bake = value;  // takes effect at the next pt_set_data
+        return PT_OK;
+    }
+    if (!std::strcmp(key, "bin_samples")) {
+        if (value < 64) return fail(c, PT_ERR_INVALID, "bin_samples must be >= 64");
+        c->bin_samples = value;
         return PT_OK;
     }
     if (!std::strcmp(key, "shade_batch")) {
@@ -623,6 +774,8 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "jit_seconds")) *value = c->jit_seconds;
     else if (!std::strcmp(key, "kernel")) *value = c->kernel;
     else if (!std::strcmp(key, "shade_batch")) *value = c->shade_batch;
+    else if (!std::strcmp(key, "bin_samples")) *value = double(bin_samples(c));
+    else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * kBinBytesPerSample;
     else return fail(c, PT_ERR_INVALID, std::string("unknown option ") + key);
     return PT_OK;
 }
@@ -643,6 +796,7 @@ void pt_destroy(pt_ctx *c) {
     (void)hipFree(c->d_aabbs);
     (void)hipFree(c->d_mats);
     (void)hipFree(c->d_stats);
+    free_bin(c);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);

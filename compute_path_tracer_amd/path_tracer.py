@@ -126,7 +126,7 @@ class PathTracer:
                                                                   ctypes.byref(self.settings), spp, buf))
         return dict(zip(N.STAT_NAMES, (int(v) for v in buf)))
 
-    KERNELS = {"auto": 0, "simple": 1, "wave": 2, "jit": 2}
+    KERNELS = {"auto": 0, "simple": 1, "wave": 2, "jit": 2, "binned": 3}
 
     def set_option(self, key: str, value) -> None:
         if key == "kernel" and isinstance(value, str):

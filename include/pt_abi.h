@@ -175,7 +175,7 @@ int pt_sync(pt_ctx *ctx);
 int pt_last_dispatch_ms(pt_ctx *ctx, float *ms);
 /* Instrumented re-run of one dispatch (does not touch the image): per-event
  * work counters for algorithmic-flop accounting. */
-#define PT_STAT_COUNT 24
+#define PT_STAT_COUNT 32
 int pt_dispatch_stats(pt_ctx *ctx, const pt_constants *c, const pt_settings *s, uint32_t spp,
                       uint64_t counters[PT_STAT_COUNT]);
 /* Tuning knobs: "kernel" (0 auto, 1 simple one-path-per-lane, 2 wavefront

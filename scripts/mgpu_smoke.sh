@@ -1,7 +1,7 @@
 #!/bin/bash
 # Multi-rank rehearsal on a single-GPU box: NPROC ranks share GPU 0. RCCL
 # refuses duplicate devices, so the image reduce goes over gloo on the host;
-# --validate checks the assembled image against a 1-GPU render bit for bit).
+# --validate checks the assembled image against a 1-GPU render bit for bit.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

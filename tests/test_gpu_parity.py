@@ -20,18 +20,22 @@ RMS_TOL = 1e-5
 
 
 KERNELS = {"simple": {"kernel": "simple", "jit": 0}, "wave": {"kernel": "wave", "jit": 0},
-           "jit": {"kernel": "wave", "jit": 1}}
+           "jit": {"kernel": "wave", "jit": 1}, "binned": {"kernel": "binned", "jit": 0},
+           "binned_jit": {"kernel": "binned", "jit": 1}}
+ALL = ["simple", "wave", "jit", "binned", "binned_jit"]
 
 
 def _render_pair(ed, w, h, spp, bounces, debug=0, frame=1, last_clear=1, fov=1.0, aspect=None, kernel="jit",
-                 shade_batch=None):
+                 shade_batch=None, bin_samples=None):
     prog = ed.compile(CompData())
     st = N.Settings(debug=debug, bounces=bounces, scale=1.0, fov=fov, aabb=0)
     opts = dict(KERNELS[kernel])
     if shade_batch:
         opts["shade_batch"] = shade_batch
+    if bin_samples:
+        opts["bin_samples"] = bin_samples
     pt = PathTracer(w, h, prog, settings=st, options=opts)
-    if kernel == "jit":
+    if opts["jit"]:
         assert pt.get_option("jit_active") == 1.0, pt.jit_log()
     a = float(np.float32(w) / np.float32(h)) if aspect is None else aspect
     pt.dispatch(N.Constants(time=0.0, frame=frame, aspect=a, last_clear=last_clear), spp)
@@ -51,7 +55,7 @@ def _report(gpu, ref):
     return rms, exact
 
 
-@pytest.mark.parametrize("kernel", ["simple", "wave", "jit"])
+@pytest.mark.parametrize("kernel", ALL)
 @pytest.mark.parametrize("name,w,h,spp,bounces", [
     ("c1", 256, 256, 1, 1),        # BASELINE config 1 in full
     ("c2", 96, 64, 4, 4),
@@ -67,7 +71,7 @@ def test_parity_path_trace(gpu, name, w, h, spp, bounces, kernel):
     assert exact == 1.0
 
 
-@pytest.mark.parametrize("kernel", ["simple", "wave", "jit"])
+@pytest.mark.parametrize("kernel", ALL)
 @pytest.mark.parametrize("debug", [1, 2, 3])
 def test_parity_debug_views(gpu, debug, kernel):
     gpu_img, ref = _render_pair(scenes.c3_graph32(), 80, 45, 2, 8, debug=debug, kernel=kernel)
@@ -75,7 +79,7 @@ def test_parity_debug_views(gpu, debug, kernel):
     assert rms < RMS_TOL and exact == 1.0
 
 
-@pytest.mark.parametrize("kernel", ["wave", "jit"])
+@pytest.mark.parametrize("kernel", ["wave", "jit", "binned", "binned_jit"])
 @pytest.mark.parametrize("shade_batch", [1, 7, 64])
 def test_wave_kernel_schedule_invariance(gpu, shade_batch, kernel):
     """Shading batch size changes the schedule only, never the result; spp
@@ -85,22 +89,35 @@ def test_wave_kernel_schedule_invariance(gpu, shade_batch, kernel):
     assert exact == 1.0, (shade_batch, rms)
 
 
-def test_long_dispatch_chunks(gpu):
+@pytest.mark.parametrize("kernel", ["jit", "binned_jit"])
+def test_long_dispatch_chunks(gpu, kernel):
     """spp > 64 is split into several launches that continue frame/last_clear."""
-    gpu_img, ref = _render_pair(scenes.c1_default(), 16, 16, 70, 1)
+    gpu_img, ref = _render_pair(scenes.c1_default(), 16, 16, 70, 1, kernel=kernel)
     rms, exact = _report(gpu_img, ref)
     assert exact == 1.0
 
 
-def test_empty_scene_is_black(gpu):
-    gpu_img, ref = _render_pair(scenes.empty(), 40, 24, 2, 4)
+@pytest.mark.parametrize("bin_samples", [64, 1000, 4096, 1 << 20])
+def test_binned_sub_chunks(gpu, bin_samples):
+    """The binned pipeline splits a dispatch into sub-chunks of frames that fit
+    its sample budget (one frame when the budget is below the pixel count);
+    the fold continues last_clear across them."""
+    gpu_img, ref = _render_pair(scenes.c3_graph32(), 40, 24, 11, 8, kernel="binned_jit", bin_samples=bin_samples)
+    rms, exact = _report(gpu_img, ref)
+    assert exact == 1.0, rms
+
+
+@pytest.mark.parametrize("kernel", ["jit", "binned_jit"])
+def test_empty_scene_is_black(gpu, kernel):
+    gpu_img, ref = _render_pair(scenes.empty(), 40, 24, 2, 4, kernel=kernel)
     assert np.all(gpu_img[..., :3] == 0) and np.all(gpu_img[..., 3] == 1)
     assert np.array_equal(gpu_img, ref)
 
 
-def test_ragged_and_edge_sizes(gpu):
+@pytest.mark.parametrize("kernel", ["jit", "binned_jit"])
+def test_ragged_and_edge_sizes(gpu, kernel):
     for (w, h) in [(1, 1), (7, 3), (9, 17), (65, 1)]:
-        gpu_img, ref = _render_pair(scenes.c2_sphere_box_torus(), w, h, 2, 3)
+        gpu_img, ref = _render_pair(scenes.c2_sphere_box_torus(), w, h, 2, 3, kernel=kernel)
         rms, exact = _report(gpu_img, ref)
         assert exact == 1.0, (w, h)
 
@@ -124,7 +141,8 @@ def test_progressive_equals_batched(gpu):
     assert a.constants.frame == b.constants.frame == 5
 
 
-def test_tiles_union_is_full_image(gpu):
+@pytest.mark.parametrize("kernel", ["jit", "binned_jit"])
+def test_tiles_union_is_full_image(gpu, kernel):
     ed = scenes.c3_graph32()
     prog = ed.compile(CompData())
     st = N.Settings(debug=0, bounces=8, scale=1.0, fov=1.0, aabb=0)
@@ -134,7 +152,7 @@ def test_tiles_union_is_full_image(gpu):
     ref = full.read_image()
     acc = np.zeros_like(ref)
     for r in range(3):
-        p = PathTracer(72, 40, prog, settings=st)
+        p = PathTracer(72, 40, prog, settings=st, options=KERNELS[kernel])
         p.set_tiles(r, 3)
         p.dispatch(c, 2)
         acc += p.read_image()
@@ -184,7 +202,7 @@ def test_value_update_without_recompile(gpu):
     assert np.array_equal(gpu_img.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("kernel", ["simple", "wave", "jit"])
+@pytest.mark.parametrize("kernel", ALL)
 def test_work_counters_match_oracle(gpu, kernel):
     ed = scenes.c3_graph32()
     prog = ed.compile(CompData())
