@@ -61,7 +61,7 @@ struct pt_ctx {
     int shade_batch = -1;  // -1 = environment / default
     int jit = -1;          // 1 use per-scene hipRTC kernels, 0 interpreter; -1 = env (PT_JIT), default 1
     int jit_bake = -1;     // 1 bake node values as literals; -1 = env (PT_JIT_BAKE), default 0
-    int bin_samples = -1;  // binned pipeline: samples per chunk; -1 = env (PT_BIN_SAMPLES), default 2^25
+    int bin_samples = -1;  // binned pipeline: samples per chunk; -1 = env (PT_BIN_SAMPLES), default 2^27
     PtJitModule jit_mod;   // loaded scene kernel (key = its source)
     // binned pipeline buffers (pt_binned.h), for bin_cap samples per chunk
     PtRay *d_ray[2] = {nullptr, nullptr};  // unbinned, binned
@@ -419,7 +419,7 @@ static size_t bin_samples(const pt_ctx *c) {
         const char *v = std::getenv("PT_BIN_SAMPLES");
         return v ? std::atol(v) : 0L;
     }();
-    return env >= 64 ? size_t(env) : (size_t(1) << 25);
+    return env >= 64 ? size_t(env) : (size_t(1) << 27);  // 22.5 GB of HBM; larger chunks shorten per-pass tails
 }
 
 static void free_bin(pt_ctx *c) {
@@ -603,7 +603,10 @@ static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, u
         return v ? std::atoi(v) : 0;
     }();
     L.kernel = c->kernel >= 0 ? c->kernel : env_kernel;
-    L.shade_batch = c->shade_batch > 0 ? c->shade_batch : (env_batch > 0 ? env_batch : 16);
+    if (L.kernel == PT_KERNEL_AUTO) L.kernel = PT_KERNEL_BINNED;
+    // measured defaults: binned 12, tile-resident wavefront 16
+    L.shade_batch = c->shade_batch > 0 ? c->shade_batch
+                                       : (env_batch > 0 ? env_batch : (L.kernel == PT_KERNEL_BINNED ? 12 : 16));
     return PT_OK;
 }
 

@@ -178,15 +178,20 @@ int pt_last_dispatch_ms(pt_ctx *ctx, float *ms);
 #define PT_STAT_COUNT 32
 int pt_dispatch_stats(pt_ctx *ctx, const pt_constants *c, const pt_settings *s, uint32_t spp,
                       uint64_t counters[PT_STAT_COUNT]);
-/* Tuning knobs: "kernel" (0 auto, 1 simple one-path-per-lane, 2 wavefront
- * state machine), "shade_batch" (wavefront kernel: lanes that must wait
- * before a shading pass runs, 1..64) and "jit" (1: per-scene hipRTC build of
- * the wavefront kernel, compiled at pt_set_data when the topology or an
- * identity flag changed -- the analogue of remake_pipeline; 0: op-list
- * interpreter).  Results are bit-identical for every value. */
+/* Tuning knobs: "kernel" (0 auto = 3, 1 simple one-path-per-lane, 2 tile-
+ * resident wavefront state machine, 3 mask-binned passes: per bounce, the
+ * rays of a chunk of frames are grouped by their bounds() check set before
+ * they are marched), "shade_batch" (state-machine kernels: lanes that must
+ * wait before a shading pass runs, 1..64), "bin_samples" (binned kernel:
+ * samples per chunk, >= 64; device memory = 180 B per sample) and "jit" (1:
+ * per-scene hipRTC build of the state-machine kernels, compiled at
+ * pt_set_data when the topology or an identity flag changed -- the analogue
+ * of remake_pipeline; 0: op-list interpreter).  Results are bit-identical for
+ * every value. */
 int pt_set_option(pt_ctx *ctx, const char *key, int value);
 /* Read back: "jit_active" (1 when the scene-specialised kernel is loaded),
- * "jit_seconds" (last hipRTC compile time), "kernel", "shade_batch". */
+ * "jit_seconds" (last hipRTC compile time), "kernel", "shade_batch",
+ * "bin_samples", "bin_bytes" (device memory held by the binned pipeline). */
 int pt_get_option(pt_ctx *ctx, const char *key, double *value);
 /* Log of the last failed scene-kernel build ("" if none). */
 const char *pt_jit_log(const pt_ctx *ctx);
