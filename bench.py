@@ -46,6 +46,13 @@ W_CAMERA = 25
 W_ACCUM = 10
 
 
+def trace_flops(st: dict) -> float:
+    """The part of algorithmic_flops() done by the march/normal/shade kernel
+    (the binned pipeline's trace passes): everything but bounds() and the
+    camera ray / accumulation (gen, bounds and fold kernels)."""
+    return algorithmic_flops(st) - W_AABB * st["aabb_tests"] - (W_CAMERA + W_ACCUM) * st["samples"]
+
+
 def algorithmic_flops(st: dict) -> float:
     xf = st["xform_union"] + st["xform_shape"]
     f = W_XFORM * xf + W_FINALISE * xf
@@ -188,12 +195,20 @@ def main() -> None:
         step()
     pt.sync()
     barrier()
-    kernel_ms = []
+    kernel_ms, trace_ms, trace_n = [], [], []
+
+    def record_times():
+        kernel_ms.append(pt.last_dispatch_ms())  # whole dispatch (all pipeline kernels)
+        n = int(pt.get_option("trace_launches"))
+        if n:  # binned pipeline: the trace passes, timed by events on the library stream
+            trace_ms.append(pt.get_option("trace_ms"))
+            trace_n.append(n)
+
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         if world == 1:
-            kernel_ms.append(pt.last_dispatch_ms())
+            record_times()
     pt.sync()
     barrier()
     dt = time.perf_counter() - t0
@@ -206,7 +221,7 @@ def main() -> None:
     if world > 1:
         # per-launch kernel time on this rank (events on the library stream)
         tr.step(args.spp)
-        kernel_ms.append(pt.last_dispatch_ms())
+        record_times()
     validation = None
     if args.validate:
         img = tr.image(0)  # every frame rendered so far, assembled on rank 0
@@ -229,12 +244,23 @@ def main() -> None:
             dist.destroy_process_group()
         return
 
-    k_ms = float(np.mean(kernel_ms))
-    flops_per_launch = algorithmic_flops(st)
+    d_ms = float(np.mean(kernel_ms))  # one dispatch = one step's frames of this rank
+    flops_step = algorithmic_flops(st)
     rank_pixels = st["samples"] / max(1, spp_step)
-    bytes_per_launch = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per launch
-    achieved_tf = flops_per_launch / (k_ms * 1e-3) / 1e12
-    achieved_gbs = bytes_per_launch / (k_ms * 1e-3) / 1e9
+    bytes_per_launch = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per dispatch
+    jit = bool(pt.get_option("jit_active"))
+    if trace_n:  # dominant kernel: the binned trace pass (flops of its passes / their device time)
+        hot = "pt_bin_trace_jit" if jit else "pt_bin_trace_kernel"
+        launches = float(np.mean(trace_n))
+        t_ms = float(np.mean(trace_ms))
+        k_ms = t_ms / launches
+        achieved_tf = trace_flops(st) / (t_ms * 1e-3) / 1e12
+    else:  # the tile-resident kernels do the whole path in one launch
+        hot = "pt_wave_jit" if jit else "pt_wave_kernel"
+        launches, t_ms, k_ms = 1.0, d_ms, d_ms
+        achieved_tf = flops_step / (d_ms * 1e-3) / 1e12
+    path_tf = flops_step / (d_ms * 1e-3) / 1e12
+    achieved_gbs = bytes_per_launch / (d_ms * 1e-3) / 1e9
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -252,17 +278,20 @@ def main() -> None:
                                f"{args.spp * world} spp per step ({args.spp} per GPU-share), progressive accumulate",
                    "width": args.width, "height": args.height, "bounces": args.bounces,
                    "spp_per_step": args.spp * world, "parallelism": f"tiles{world}"},
-        "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_TFLOPS,
+        "roofline": {"bound": "valu", "kernel": hot, "achieved": round(achieved_tf, 3), "peak": PEAK_F32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_TFLOPS, 4), "traffic": None,
                      "traffic_source": None,
-                     "algorithmic_flops_per_sample": round(flops_per_launch / max(1, st["samples"]), 1),
+                     "algorithmic_flops_per_sample": round(flops_step / max(1, st["samples"]), 1),
+                     "kernel_flops_per_launch": round((trace_flops(st) if trace_n else flops_step) / launches),
                      "frac_nonpacked": round(achieved_tf / PEAK_F32_TFLOPS_NONPACKED, 4),
-                     "kernel_ms_per_launch": round(k_ms, 3)},
+                     "kernel_ms_per_launch": round(k_ms, 3), "kernel_launches_per_step": launches,
+                     "dispatch_ms_per_step": round(d_ms, 3),
+                     "path_achieved": round(path_tf, 3), "path_frac": round(path_tf / PEAK_F32_TFLOPS, 4)},
         "hbm": {"achieved": round(achieved_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "algorithmic_bytes_per_launch": bytes_per_launch},
         "work": st,
         "schedule": schedule_metrics(st),
-        "jit": {"active": bool(pt.get_option("jit_active")), "compile_s": round(pt.get_option("jit_seconds"), 3)},
+        "jit": {"active": jit, "compile_s": round(pt.get_option("jit_seconds"), 3)},
     }
     if validation is not None:
         out["validation"] = validation

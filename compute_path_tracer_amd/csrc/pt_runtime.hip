@@ -70,6 +70,9 @@ struct pt_ctx {
     float4 *d_color = nullptr;
     size_t bin_cap = 0, ctrl_words = 0;
     int cu_count = 0;
+    // HIP events around each trace-pass launch of the last dispatch (pairs)
+    std::vector<hipEvent_t> tev;
+    size_t tev_used = 0;
     std::string jit_log;
     double jit_seconds = 0.0;
     std::string err;
@@ -465,6 +468,16 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes) {
     return PT_OK;
 }
 
+static hipError_t record_trace_event(pt_ctx *c) {
+    if (c->tev_used == c->tev.size()) {
+        hipEvent_t e;
+        const hipError_t err = hipEventCreate(&e);
+        if (err != hipSuccess) return err;
+        c->tev.push_back(e);
+    }
+    return hipEventRecord(c->tev[c->tev_used++], c->stream);
+}
+
 // One dispatch chunk through the pass pipeline: frames are processed in
 // sub-chunks of at most bin_samples() samples.
 static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
@@ -531,6 +544,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             pt_launch_bin(PtBinStage::Scan, P, stats, 1, c->stream);
             pt_launch_bin(PtBinStage::Scatter, P, stats, scatter_grid(k == 0 ? n0 : c->bin_cap), c->stream);
             HIPCHK(c, hipGetLastError());
+            if (!stats) HIPCHK(c, record_trace_event(c));
             if (jit) {
                 void *args[] = {&P};
                 HIPCHK(c, hipModuleLaunchKernel(jf, trace_grid, 1, 1, 64, 1, 1, 0, c->stream, args, nullptr));
@@ -538,6 +552,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 pt_launch_bin(PtBinStage::Trace, P, stats, trace_grid, c->stream);
                 HIPCHK(c, hipGetLastError());
             }
+            if (!stats) HIPCHK(c, record_trace_event(c));
         }
         pt_launch_bin(PtBinStage::Fold, P, stats, unsigned((n_pix + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK), c->stream);
         HIPCHK(c, hipGetLastError());
@@ -616,6 +631,7 @@ int pt_dispatch(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t
     if (rc != PT_OK) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    c->tev_used = 0;
     if (spp > 0 && L.n_tiles > 0) {
         // bound a single launch's length; chunks continue frame/last_clear
         const uint32_t chunk = 64;
@@ -778,6 +794,17 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "kernel")) *value = c->kernel;
     else if (!std::strcmp(key, "shade_batch")) *value = c->shade_batch;
     else if (!std::strcmp(key, "bin_samples")) *value = double(bin_samples(c));
+    else if (!std::strcmp(key, "trace_launches")) *value = double(c->tev_used / 2);
+    else if (!std::strcmp(key, "trace_ms")) {  // summed device time of the last dispatch's trace passes
+        double sum = 0.0;
+        if (c->tev_used) HIPCHK(c, hipEventSynchronize(c->tev[c->tev_used - 1]));
+        for (size_t i = 0; i + 1 < c->tev_used; i += 2) {
+            float ms = 0.0f;
+            HIPCHK(c, hipEventElapsedTime(&ms, c->tev[i], c->tev[i + 1]));
+            sum += ms;
+        }
+        *value = sum;
+    }
     else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * kBinBytesPerSample;
     else return fail(c, PT_ERR_INVALID, std::string("unknown option ") + key);
     return PT_OK;
@@ -802,6 +829,7 @@ void pt_destroy(pt_ctx *c) {
     free_bin(c);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -191,7 +191,9 @@ int pt_dispatch_stats(pt_ctx *ctx, const pt_constants *c, const pt_settings *s, 
 int pt_set_option(pt_ctx *ctx, const char *key, int value);
 /* Read back: "jit_active" (1 when the scene-specialised kernel is loaded),
  * "jit_seconds" (last hipRTC compile time), "kernel", "shade_batch",
- * "bin_samples", "bin_bytes" (device memory held by the binned pipeline). */
+ * "bin_samples", "bin_bytes" (device memory held by the binned pipeline),
+ * "trace_ms" / "trace_launches" (device time and count of the last dispatch's
+ * binned trace passes, HIP events on the context stream). */
 int pt_get_option(pt_ctx *ctx, const char *key, double *value);
 /* Log of the last failed scene-kernel build ("" if none). */
 const char *pt_jit_log(const pt_ctx *ctx);

@@ -7,9 +7,10 @@ metrics) and profiles/<tag>_summary.md.
 
 HBM bytes per launch follow MI355X_MICROARCH.md "HBM": FETCH_SIZE reads
 exactly half of a wide coalesced stream on gfx950 (16 B/lane loads, which is
-what the kernel's float4 texel load is), so bytes = 2*FETCH_SIZE*1024 +
-WRITE_SIZE*1024 (WRITE_SIZE is exact for 16 B/lane stores); each counter from
-its own pass.
+what the kernels' float4 ray / texel loads are), so bytes = 2*FETCH_SIZE*1024
++ WRITE_SIZE*1024 (WRITE_SIZE is exact for 16 B/lane stores); each counter
+from its own pass.  The hot kernel is the binned trace pass when present
+(averages over its launches), else the tile-resident kernel.
 """
 from __future__ import annotations
 
@@ -21,7 +22,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HOT = ("pt_wave_jit", "pt_wave_kernel", "pt_render_kernel")
+HOT = ("pt_bin_trace_jit", "pt_bin_trace_kernel", "pt_wave_jit", "pt_wave_kernel", "pt_render_kernel")
 
 
 def hot_name(name: str) -> bool:
@@ -39,11 +40,13 @@ def main(tag: str, src: str = None) -> None:
     for line in open(os.path.join(src, "kt_bench.log")):
         if line.startswith("{"):
             bench_line = json.loads(line)
+    present = [r["Name"] for r in stats if hot_name(r["Name"])]
+    hot = min(present, key=lambda n: [i for i, h in enumerate(HOT) if n.startswith(h)][0]) if present else None
     counters, launches = {}, {}
     meta = {}
     for f in sorted(glob.glob(os.path.join(src, "pmc*", "pmc_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
-            if not hot_name(r["Kernel_Name"]):
+            if r["Kernel_Name"] != hot:
                 continue
             k = r["Counter_Name"]
             counters[k] = counters.get(k, 0.0) + float(r["Counter_Value"])
@@ -71,7 +74,7 @@ def main(tag: str, src: str = None) -> None:
         d["wave_time_waitcnt"] = c.get("SQ_WAIT_ANY", 0.0) / tot
     ktime = None
     for r in stats:
-        if hot_name(r["Name"]):
+        if r["Name"] == hot:
             ktime = float(r["AverageNs"]) * 1e-9
     if ktime and "hbm_bytes_per_launch" in d:
         d["hbm_gbs_measured"] = d["hbm_bytes_per_launch"] / ktime / 1e9
