@@ -42,7 +42,8 @@ SYMBOLS = (
     "pt_dispatch", "pt_read_accum", "pt_accum_device_ptr", "pt_get_size", "pt_comm_get_unique_id",
     "pt_comm_init", "pt_reduce_accum", "pt_read_reduced", "pt_sync", "pt_last_dispatch_ms",
     "pt_dispatch_stats", "pt_set_option", "pt_get_option", "pt_jit_log", "pt_jit_compile", "pt_last_error",
-    "pt_destroy", "pt_abi_version", "pt_device_math", "pt_check_sqrt_exhaustive",
+    "pt_destroy", "pt_abi_version", "pt_device_math", "pt_check_sqrt_exhaustive", "pt_check_div_exhaustive",
+    "pt_check_div_random",
 )
 PT_MATH = {"max": 0, "min": 1, "sqrt": 2, "sqrtf": 3, "sin": 4, "cos": 5, "div": 6, "fma": 7}
 
@@ -135,6 +136,9 @@ def lib() -> ctypes.CDLL:
         "pt_abi_version": (c_int, []),
         "pt_device_math": (c_int, [c_int, c_int, POINTER(c_float), POINTER(c_float), POINTER(c_float), c_uint32]),
         "pt_check_sqrt_exhaustive": (c_int, [c_int, POINTER(c_uint64), POINTER(c_uint32)]),
+        "pt_check_div_exhaustive": (c_int, [c_int, c_uint32, c_uint32, c_uint32, c_uint32, POINTER(c_uint64),
+                                            POINTER(c_uint64)]),
+        "pt_check_div_random": (c_int, [c_int, c_uint32, c_uint32, POINTER(c_uint64), POINTER(c_uint64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -66,13 +66,25 @@ __device__ __forceinline__ uint32_t bin_of(const uint4 &m) {
 }
 
 // bounds() of one ray, one thread: every box's slab test (scalar box loads).
+// Rays (and scenes, L.fast_bounds) inside the pt_div_*_ok guards divide via
+// per-ray reciprocals; the rest take the IEEE divisions.  Same bits either way.
 template <bool ST>
 __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro, const pt_f3 &rd, Stats<ST> &st) {
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     const caabb_ptr boxes = (caabb_ptr)L.aabbs;
-    for (int b = 0; b < L.n_aabb; ++b) {
-        const PtAabb bx = boxes[b];
-        if (ray_box(bx, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z)) w[bx.back >> 5] |= 1u << (bx.back & 31);
+    const bool fast = L.fast_bounds != 0 && pt_div_coord_ok(ro.x) && pt_div_coord_ok(ro.y) &&
+                      pt_div_coord_ok(ro.z) && pt_div_dir_ok(rd.x) && pt_div_dir_ok(rd.y) && pt_div_dir_ok(rd.z);
+    if (fast) {
+        const float yx = 1.0f / rd.x, yy = 1.0f / rd.y, yz = 1.0f / rd.z;
+        for (int b = 0; b < L.n_aabb; ++b) {
+            const PtAabb bx = boxes[b];
+            if (ray_box_rcp(bx, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, yx, yy, yz)) w[bx.back >> 5] |= 1u << (bx.back & 31);
+        }
+    } else {
+        for (int b = 0; b < L.n_aabb; ++b) {
+            const PtAabb bx = boxes[b];
+            if (ray_box(bx, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z)) w[bx.back >> 5] |= 1u << (bx.back & 31);
+        }
     }
     st.add(PT_ST_SEGMENTS);
     st.add(PT_ST_AABB, uint32_t(L.n_aabb));

@@ -121,6 +121,7 @@ struct PtLaunch {
     int32_t write;           // 0: instrumented run, leave the image untouched
     int32_t kernel;          // PT_KERNEL_* (0 = choose)
     int32_t shade_batch;     // wavefront kernel: shade when >= this many lanes wait
+    int32_t fast_bounds;     // every box coordinate passes pt_div_coord_ok (reciprocal slab divisions allowed)
 };
 
 #define PT_KERNEL_AUTO 0

@@ -109,6 +109,29 @@ PT_HD float pt_sqrt(float x) {
 #endif
 }
 
+// Correctly rounded a / b from y = RN(1/b) with one residual correction
+// (Markstein): q = RN(a*y), r = a - q*b (exact by fma), RN(q + r*y).  Equal
+// to IEEE a / b whenever nothing under/overflows; bounds() takes it under the
+// guards below, which keep every intermediate normal.
+// Proven on the device for every pair of significands (pt_check_div_exhaustive)
+// -- power-of-two scaling carries that to all guarded exponents.
+PT_HD float pt_div_rcp(float a, float b, float y) {
+    const float q = a * y;
+    const float r = fmaf(-q, b, a);
+    return fmaf(r, y, q);
+}
+// slab operand guard: 0 or |x| in [2^-36, 2^59] (then a difference of two
+// such values is 0 or in [2^-60, 2^60])
+PT_HD bool pt_div_coord_ok(float x) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, x) & 0x7fffffffu;
+    return u == 0u || (u - 0x2D800000u) <= (0x5D000000u - 0x2D800000u);
+}
+// divisor guard: |d| in [2^-20, 2^59]
+PT_HD bool pt_div_dir_ok(float d) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, d) & 0x7fffffffu;
+    return (u - 0x35800000u) <= (0x5D000000u - 0x35800000u);
+}
+
 struct pt_f3 {
     float x, y, z;
 };

@@ -39,6 +39,19 @@ __device__ __forceinline__ bool ray_box(const PtAabb &bx, float ox, float oy, fl
     return tnear < tfar && tfar > 0.0f;
 }
 
+// The same test with the divisions as pt_div_rcp from per-ray reciprocals
+// (y = RN(1/d)); bit-identical results when the pt_div_*_ok guards hold for
+// the ray and the box (bounds_fast in pt_binned.h).
+__device__ __forceinline__ bool ray_box_rcp(const PtAabb &bx, float ox, float oy, float oz, float dx, float dy,
+                                            float dz, float yx, float yy, float yz) {
+    const float tminx = pt_div_rcp(bx.bmin[0] - ox, dx, yx), tmaxx = pt_div_rcp(bx.bmax[0] - ox, dx, yx);
+    const float tminy = pt_div_rcp(bx.bmin[1] - oy, dy, yy), tmaxy = pt_div_rcp(bx.bmax[1] - oy, dy, yy);
+    const float tminz = pt_div_rcp(bx.bmin[2] - oz, dz, yz), tmaxz = pt_div_rcp(bx.bmax[2] - oz, dz, yz);
+    const float tnear = pt_gmax(pt_gmax(pt_gmin(tminx, tmaxx), pt_gmin(tminy, tmaxy)), pt_gmin(tminz, tmaxz));
+    const float tfar = pt_gmin(pt_gmin(pt_gmax(tminx, tmaxx), pt_gmax(tminy, tmaxy)), pt_gmax(tminz, tmaxz));
+    return tnear < tfar && tfar > 0.0f;
+}
+
 // The map() argument of a lane: CastRay's p = ro + rd*t (MARCH), or normal
 // tap `step` (0..5 = +x,-x,+y,-y,+z,-z) around the hit point held in ro
 // (calc_normal, test_compute.glsl:57-66).

@@ -70,6 +70,7 @@ struct pt_ctx {
     float4 *d_color = nullptr;
     size_t bin_cap = 0, ctrl_words = 0;
     int cu_count = 0;
+    bool fast_bounds = false;  // every box coordinate inside the reciprocal-division guard
     // HIP events around each trace-pass launch of the last dispatch (pairs)
     std::vector<hipEvent_t> tev;
     size_t tev_used = 0;
@@ -400,6 +401,10 @@ int pt_set_data(pt_ctx *c, const float *data, uint32_t n) {
     HIPCHK(c, hipMemcpyAsync(c->d_mats, mats.data(), mats.size() * sizeof(PtMat), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->have_data = true;
+    c->fast_bounds = true;
+    for (const PtAabb &b : boxes)
+        for (int k = 0; k < 3; ++k)
+            if (!pt_div_coord_ok(b.bmin[k]) || !pt_div_coord_ok(b.bmax[k])) c->fast_bounds = false;
     jit_refresh(c, nodes);
     return PT_OK;
 }
@@ -585,6 +590,7 @@ static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, u
     std::memset(&L, 0, sizeof L);
     L.nodes = c->d_nodes;
     L.aabbs = c->d_aabbs;
+    L.fast_bounds = c->fast_bounds ? 1 : 0;
     L.mats = c->d_mats;
     L.accum = c->accum;
     L.n_nodes = int32_t(c->ops.size());

@@ -1,9 +1,13 @@
 // pt_selftest.hip -- device arithmetic probes for the semantics contract
 // (DESIGN.md 3): the tests compare the GPU's min/max/sqrt/sin/cos/divide on
-// chosen operands with the host restatements, and check the kernels' fast
+// chosen operands with the host restatements, check the kernels' fast
 // correctly-rounded sqrt against the compiler's IEEE sqrtf for every one of
-// the 2^32 f32 bit patterns.
+// the 2^32 f32 bit patterns, and the reciprocal-based division of bounds()
+// (pt_div_rcp) against IEEE division for every pair of significands plus
+// random guarded operands.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "../../include/pt_abi.h"
 #include "pt_math.h"
@@ -55,7 +59,108 @@ __global__ void sqrt_sweep(uint64_t base, uint32_t count, unsigned long long *ba
     if (nbad) atomicAdd(bad, nbad);
 }
 
+// pt_div_rcp vs IEEE a / b for a = 1.ma, b = 1.mb over a block of
+// significands: one b per thread, a looping.  The first mismatch is kept as
+// (b bits << 32 | a bits).
+__global__ void div_sweep(uint32_t a0, uint32_t na, uint32_t b0, uint32_t nb, unsigned long long *bad,
+                          unsigned long long *first) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nb) return;
+    const float b = __uint_as_float(0x3F800000u | (b0 + i));
+    const float y = 1.0f / b;
+    unsigned long long nbad = 0;
+    for (uint32_t k = 0; k < na; ++k) {
+        const float a = __uint_as_float(0x3F800000u | (a0 + k));
+        const float got = pt_div_rcp(a, b, y), want = a / b;
+        if (__float_as_uint(got) != __float_as_uint(want)) {
+            ++nbad;
+            atomicMin(first, (static_cast<unsigned long long>(__float_as_uint(b)) << 32) | __float_as_uint(a));
+        }
+    }
+    if (nbad) atomicAdd(bad, nbad);
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+// random slab operand inside the guard: 0 (1/16) or sign * 2^[-36, 58] * 1.m
+__device__ __forceinline__ float guard_coord(uint32_t h, uint32_t m) {
+    if ((h & 15u) == 0u) return (h & 16u) ? -0.0f : 0.0f;
+    const uint32_t e = 91u + (h >> 8) % 95u;  // [2^-36, 2^59)
+    return __uint_as_float(((h & 32u) << 26) | (e << 23) | (m & 0x7fffffu));
+}
+// random divisor inside the guard: sign * 2^[-20, 58] * 1.m, or exactly +-1
+__device__ __forceinline__ float guard_dir(uint32_t h, uint32_t m) {
+    if ((h & 63u) == 0u) return (h & 64u) ? -1.0f : 1.0f;
+    const uint32_t e = 107u + (h >> 8) % 79u;
+    return __uint_as_float(((h & 128u) << 24) | (e << 23) | (m & 0x7fffffu));
+}
+// The composed bounds() claim: a = x - o for guarded x, o; guarded d; then
+// pt_div_rcp(a, d, 1/d) == a / d, except that a zero quotient may differ in
+// sign (which no slab comparison can observe).
+__global__ void div_random(uint32_t seed, uint32_t n, unsigned long long *bad, unsigned long long *first) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t h0 = mix32(seed ^ mix32(i * 4u)), h1 = mix32(h0 + 1u), h2 = mix32(h0 + 2u), h3 = mix32(h0 + 3u);
+    const float x = guard_coord(h0, h1), o = guard_coord(h1 * 3u + 7u, h2), d = guard_dir(h2 * 5u + 1u, h3);
+    const float a = x - o;
+    const float got = pt_div_rcp(a, d, 1.0f / d), want = a / d;
+    const bool same = __float_as_uint(got) == __float_as_uint(want) || (got == 0.0f && want == 0.0f);
+    if (!same || !pt_div_coord_ok(x) || !pt_div_coord_ok(o) || !pt_div_dir_ok(d)) {
+        atomicAdd(bad, 1ull);
+        atomicMin(first, (static_cast<unsigned long long>(__float_as_uint(d)) << 32) | __float_as_uint(a));
+    }
+}
+
 }  // namespace
+
+extern "C" int pt_check_div_exhaustive(int hip_device, uint32_t a0, uint32_t na, uint32_t b0, uint32_t nb,
+                                       uint64_t *mismatches, uint64_t *first_bad) {
+    if (!mismatches || !first_bad || a0 + uint64_t(na) > (1u << 23) || b0 + uint64_t(nb) > (1u << 23))
+        return PT_ERR_INVALID;
+    if (hipSetDevice(hip_device) != hipSuccess) return PT_ERR_HIP;
+    unsigned long long *d = nullptr;
+    if (hipMalloc(&d, 2 * sizeof(*d)) != hipSuccess) return PT_ERR_HIP;
+    const unsigned long long init[2] = {0ull, ~0ull};
+    int rc = hipMemcpy(d, init, sizeof init, hipMemcpyHostToDevice) == hipSuccess ? PT_OK : PT_ERR_HIP;
+    // slices of a keep each launch well under a second
+    for (uint32_t a = a0; rc == PT_OK && a < a0 + na; a += 1u << 15) {
+        const uint32_t cnt = std::min<uint32_t>(1u << 15, a0 + na - a);
+        hipLaunchKernelGGL(div_sweep, dim3((nb + 255) / 256), dim3(256), 0, 0, a, cnt, b0, nb, d, d + 1);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = PT_ERR_HIP;
+    }
+    unsigned long long h[2] = {0ull, 0ull};
+    if (rc == PT_OK && hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) rc = PT_ERR_HIP;
+    *mismatches = h[0];
+    *first_bad = h[1];
+    (void)hipFree(d);
+    return rc;
+}
+
+extern "C" int pt_check_div_random(int hip_device, uint32_t seed, uint32_t n, uint64_t *mismatches,
+                                   uint64_t *first_bad) {
+    if (!mismatches || !first_bad) return PT_ERR_INVALID;
+    if (hipSetDevice(hip_device) != hipSuccess) return PT_ERR_HIP;
+    unsigned long long *d = nullptr;
+    if (hipMalloc(&d, 2 * sizeof(*d)) != hipSuccess) return PT_ERR_HIP;
+    const unsigned long long init[2] = {0ull, ~0ull};
+    int rc = hipMemcpy(d, init, sizeof init, hipMemcpyHostToDevice) == hipSuccess ? PT_OK : PT_ERR_HIP;
+    if (rc == PT_OK && n > 0) {
+        hipLaunchKernelGGL(div_random, dim3((n + 255) / 256), dim3(256), 0, 0, seed, n, d, d + 1);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = PT_ERR_HIP;
+    }
+    unsigned long long h[2] = {0ull, 0ull};
+    if (rc == PT_OK && hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) rc = PT_ERR_HIP;
+    *mismatches = h[0];
+    *first_bad = h[1];
+    (void)hipFree(d);
+    return rc;
+}
 
 extern "C" int pt_device_math(int hip_device, int op, const float *a, const float *b, float *out, uint32_t n) {
     if (!a || !b || !out) return PT_ERR_INVALID;

@@ -218,6 +218,15 @@ int pt_abi_version(void);
 int pt_device_math(int hip_device, int op, const float *a, const float *b, float *out, uint32_t n);
 /* The kernels' sqrt vs IEEE sqrtf over all 2^32 inputs (NaN payloads aside). */
 int pt_check_sqrt_exhaustive(int hip_device, uint64_t *mismatches, uint32_t *first_bad);
+/* bounds()' reciprocal division (q = a*y, r = fma(-q,b,a), fma(r,y,q) with
+ * y = 1/b) vs IEEE a / b for every a = 1.(a0..a0+na-1), b = 1.(b0..b0+nb-1)
+ * significand pair (na, nb <= 2^23); first_bad = b bits << 32 | a bits. */
+int pt_check_div_exhaustive(int hip_device, uint32_t a0, uint32_t na, uint32_t b0, uint32_t nb,
+                            uint64_t *mismatches, uint64_t *first_bad);
+/* The same on n random operands drawn inside the bounds() guards (a = x - o
+ * of two guarded coordinates, guarded divisor); a zero quotient may differ in
+ * sign only. */
+int pt_check_div_random(int hip_device, uint32_t seed, uint32_t n, uint64_t *mismatches, uint64_t *first_bad);
 
 #ifdef __cplusplus
 }

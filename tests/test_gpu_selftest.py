@@ -70,3 +70,23 @@ def test_fma_is_fused(gpu):
     a = np.float32(1.0000001)
     got = dev("fma", np.array([a], np.float32), np.array([a], np.float32))[0]
     assert got == pyref.fmaf(a, a, np.float32(1.0))
+
+
+def test_div_rcp_equals_ieee_div_for_all_significand_pairs(gpu):
+    """bounds()' reciprocal division against IEEE division for all 2^46 pairs
+    of significands (a, b in [1, 2)); with no under/overflow -- what the
+    bounds() guards ensure -- power-of-two scaling and sign symmetry carry the
+    result to every guarded operand."""
+    bad, first = ctypes.c_uint64(), ctypes.c_uint64()
+    assert N.lib().pt_check_div_exhaustive(0, 0, 1 << 23, 0, 1 << 23, ctypes.byref(bad), ctypes.byref(first)) == N.PT_OK
+    assert bad.value == 0, hex(first.value)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_div_rcp_on_guarded_operands(gpu, seed):
+    """The composed claim on 2^28 random guarded operands per seed: slab
+    differences a = x - o of guarded coordinates (zeros included) over guarded
+    divisors."""
+    bad, first = ctypes.c_uint64(), ctypes.c_uint64()
+    assert N.lib().pt_check_div_random(0, seed, 1 << 28, ctypes.byref(bad), ctypes.byref(first)) == N.PT_OK
+    assert bad.value == 0, hex(first.value)
