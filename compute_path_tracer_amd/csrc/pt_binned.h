@@ -8,13 +8,16 @@
 // over all live paths of a chunk of frames:
 //
 //   gen     camera rays of every (pixel, frame) + their bounds() mask
-//   bin     histogram of mask bins -> prefix sum -> scatter, which moves the
-//           rays (64 B) and masks into bin order
-//   trace   persistent waves take runs of the binned rays, 64 at a time into
-//           staging registers (one window prefetched ahead), and march,
-//           calc_normal and shade them; ended paths store their colour, the
-//           others write their next ray back at the same position
-//   bounds  bounds() mask + bin of every written-back ray (next pass)
+//   bin     histogram of mask bins -> prefix sum -> scatter of 4-byte ray
+//           slots into bin order
+//   trace   persistent waves take runs of the binned slots; the slots of the
+//           next 64-ray window are prefetched one window ahead, the rays
+//           (64 B records, mask included) gathered into staging registers
+//           and handed to free lanes, which march, calc_normal and shade
+//           them; ended paths store their colour, the others write their next
+//           ray to the other ray buffer at their binned position
+//   bounds  bounds() mask + bin of every written ray (next pass), with the
+//           live rays compacted per wave
 //   fold    each pixel mixes its frames' colours in frame order
 //
 // Paths are independent and the fold runs in frame order, so the schedule
@@ -35,26 +38,27 @@ struct PtRay {  // a path between two segments, 64 B
     float thr[3];
     float ret[3];
     uint32_t rng;
-    uint32_t sid;  // sample slot: frame * n_pix + local pixel; PT_BIN_NONE: path ended
-    uint32_t pad[2];
+    uint32_t sid;      // sample slot: frame * n_pix + local pixel; PT_BIN_NONE: path ended
+    uint32_t mask[2];  // check[] bits 0..63 of the segment (bits 64..127: PtPass.mask_hi)
 };
 
 struct PtPass {
     PtLaunch L;             // scene tables, image, frame0 / last_clear0 of this chunk
-    PtRay *ru;              // unbinned rays: gen's camera rays, trace's written-back next rays
-    PtRay *rs;              // the same rays in bin order (scatter -> trace)
-    uint4 *mask_u;          // check[] bits per ru slot (gen / bounds)
-    uint4 *mask_s;          // ... in bin order
-    uint32_t *key;          // bin per ru slot (PT_BIN_NONE: no live ray)
+    PtRay *rin;             // this pass's rays, by slot (gen / bounds: the rays being binned)
+    PtRay *rout;            // trace: next pass's rays, by binned position
+    uint2 *mask_hi;         // check[] bits 64..127 per rin slot (scenes with > 64 entries)
+    uint32_t *key;          // bin per rin slot (PT_BIN_NONE: no live ray)
+    uint32_t *idx;          // rin slots in bin order
     uint32_t *hist;         // [PT_BINS] counts, zero outside gen/bounds -> scan
     uint32_t *offs;         // [PT_BINS] scatter cursors
     uint32_t *ctrl;         // this pass: [0] binned rays, [1] trace run cursor
-    const uint32_t *n_src;  // ru slots (bounds / scatter), null: n_src_const
+    const uint32_t *n_src;  // rin slots (bounds / scatter), null: n_src_const
     float4 *color;          // [frames][n_pix] sample colours
     uint32_t n_src_const;
     int32_t bounce;         // segment index of this pass (path_trace's loop counter i)
     int32_t n_pix;          // local pixel slots: n_tiles * 64
     int32_t frames;         // frames in this chunk
+    int32_t wide;           // check[] has more than 64 entries
 };
 
 namespace pt {
@@ -92,25 +96,12 @@ __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro,
 }
 
 __device__ __forceinline__ void store_ray(PtRay *r, const pt_f3 &ro, const pt_f3 &rd, const pt_f3 &thr,
-                                          const pt_f3 &ret, uint32_t rng, uint32_t sid) {
+                                          const pt_f3 &ret, uint32_t rng, uint32_t sid, uint32_t m0, uint32_t m1) {
     float4 *v = reinterpret_cast<float4 *>(r);
     v[0] = make_float4(ro.x, ro.y, ro.z, rd.x);
     v[1] = make_float4(rd.y, rd.z, thr.x, thr.y);
     v[2] = make_float4(thr.z, ret.x, ret.y, ret.z);
-    reinterpret_cast<uint4 *>(r)[3] = make_uint4(rng, sid, 0u, 0u);
-}
-
-__device__ __forceinline__ void load_ray(const PtRay *r, pt_f3 &ro, pt_f3 &rd, pt_f3 &thr, pt_f3 &ret, uint32_t &rng,
-                                         uint32_t &sid) {
-    const float4 *v = reinterpret_cast<const float4 *>(r);
-    const float4 a = v[0], b = v[1], c = v[2];
-    const uint4 d = reinterpret_cast<const uint4 *>(r)[3];
-    ro = pt_f3{a.x, a.y, a.z};
-    rd = pt_f3{a.w, b.x, b.y};
-    thr = pt_f3{b.z, b.w, c.x};
-    ret = pt_f3{c.y, c.z, c.w};
-    rng = d.x;
-    sid = d.y;
+    reinterpret_cast<uint4 *>(r)[3] = make_uint4(rng, sid, m0, m1);
 }
 
 __device__ __forceinline__ void hist_zero(uint32_t *lh) {
@@ -152,9 +143,9 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
         pt_f3 ro, rd;
         camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), L.width, L.height, L.aspect, L.fov, rng, ro, rd);
         st.add(PT_ST_SAMPLES);
-        store_ray(P.ru + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, pt_f3{0.0f, 0.0f, 0.0f}, rng, i);
         const uint4 m = bounds_mask<ST>(L, ro, rd, st);
-        P.mask_u[i] = m;
+        store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, pt_f3{0.0f, 0.0f, 0.0f}, rng, i, m.x, m.y);
+        if (P.wide) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t b = bin_of(m);
         P.key[i] = b;
         atomicAdd(&lh[b], 1u);
@@ -163,28 +154,51 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
     flush_stats<ST>(L, st);
 }
 
-// bounds: mask + bin of every ray the last trace pass wrote back.
+// bounds: mask + bin of every ray the last trace pass wrote.  Each wave
+// compacts the live rays of its slots through an LDS queue, so ended paths
+// (their slots hold only the end marker) leave no lane idle.
 template <bool ST>
 __device__ __forceinline__ void bin_bounds_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
+    __shared__ uint32_t queue[PT_BIN_BLOCK / 64][128];
     hist_zero(lh);
     Stats<ST> st;
     st.init();
     const PtLaunch &L = P.L;
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const float4 *v = reinterpret_cast<const float4 *>(P.ru + i);
-        if (reinterpret_cast<const uint4 *>(v)[3].y == PT_BIN_NONE) {  // path ended in the last pass
-            P.key[i] = PT_BIN_NONE;
-            continue;
-        }
+    const int lane = int(threadIdx.x & 63u), wv = int(threadIdx.x >> 6);
+    uint32_t *q = queue[wv];
+    uint32_t qn = 0u;  // wave-uniform queue length
+    auto work = [&](uint32_t i) {
+        const float4 *v = reinterpret_cast<const float4 *>(P.rin + i);
         const float4 a = v[0], b = v[1];
         const uint4 m = bounds_mask<ST>(L, pt_f3{a.x, a.y, a.z}, pt_f3{a.w, b.x, b.y}, st);
-        P.mask_u[i] = m;
+        reinterpret_cast<uint2 *>(P.rin + i)[7] = make_uint2(m.x, m.y);
+        if (P.wide) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);
         P.key[i] = k;
         atomicAdd(&lh[k], 1u);
+    };
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + uint32_t(wv)) * 64u; base < n; base += waves * 64u) {
+        const uint32_t i = base + uint32_t(lane);
+        bool live = false;
+        if (i < n) {
+            live = P.rin[i].sid != PT_BIN_NONE;
+            if (!live) P.key[i] = PT_BIN_NONE;
+        }
+        const uint64_t lm = __ballot(live);
+        if (live) q[qn + uint32_t(lane_rank(lm))] = i;
+        qn += uint32_t(__popcll(lm));
+        __builtin_amdgcn_wave_barrier();
+        if (qn >= 64u) {
+            qn -= 64u;
+            work(q[qn + uint32_t(lane)]);
+            __builtin_amdgcn_wave_barrier();
+        }
     }
+    __builtin_amdgcn_wave_barrier();
+    if (uint32_t(lane) < qn) work(q[lane]);
     hist_flush(lh, P.hist);
     flush_stats<ST>(L, st);
 }
@@ -219,9 +233,8 @@ __device__ __forceinline__ void bin_scan_body(const PtPass &P) {
     }
 }
 
-// scatter: live rays and their masks into bin order.  Per block tile, the
-// rays of one bin take consecutive places (LDS ranks) after one global
-// reservation.
+// scatter: ray slots into bin order.  Per block tile, the slots of one bin
+// take consecutive places (LDS ranks) after one global reservation.
 __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
     __shared__ uint32_t cnt[PT_BINS];
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
@@ -241,29 +254,20 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
             if (c != 0u) cnt[b] = atomicAdd(&P.offs[b], c);
         }
         __syncthreads();
-#pragma unroll 4
+#pragma unroll
         for (int j = 0; j < PT_SCATTER_ITEMS; ++j)
-            if (kk[j] != PT_BIN_NONE) {
-                const uint32_t src = t0 + uint32_t(j * PT_BIN_BLOCK) + threadIdx.x, dst = cnt[kk[j]] + rr[j];
-                const uint4 *a = reinterpret_cast<const uint4 *>(P.ru + src);
-                uint4 *b = reinterpret_cast<uint4 *>(P.rs + dst);
-                const uint4 v0 = a[0], v1 = a[1], v2 = a[2], v3 = a[3], m = P.mask_u[src];
-                b[0] = v0;
-                b[1] = v1;
-                b[2] = v2;
-                b[3] = v3;
-                P.mask_s[dst] = m;
-            }
+            if (kk[j] != PT_BIN_NONE) P.idx[cnt[kk[j]] + rr[j]] = t0 + uint32_t(j * PT_BIN_BLOCK) + threadIdx.x;
         __syncthreads();
     }
 }
 
 // trace: one wave per block, persistent.  The wave takes runs of the binned
-// rays (so its lanes share their check[] set); within a run, windows of 64
-// rays are loaded into staging registers one window ahead and handed to free
-// lanes by cross-lane moves.  Lanes run the MARCH -> NORMAL -> SHADE state
-// machine of pt_path.h; a shaded path either ends (colour stored) or writes
-// its next ray back to ru at its binned position.
+// slots (so its lanes share their check[] set).  Windows of 64: the slots of
+// the next window are loaded one window ahead, the current window's rays are
+// gathered into staging registers and handed to free lanes by cross-lane
+// moves.  Lanes run the MARCH -> NORMAL -> SHADE state machine of pt_path.h;
+// a shaded path either ends (colour stored, end marker written) or writes
+// its next ray to rout at its binned position.
 template <class Map, bool ST>
 __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     const PtLaunch &L = P.L;
@@ -283,31 +287,44 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     uint32_t run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt))), run_end = 0u;
     run_end = run_cur < n ? (run_cur + R < n ? run_cur + R : n) : run_cur;
     if (lane == 0 && run_cur < n) nxt = atomicAdd(&P.ctrl[1], R);
-    // staging window: lane j holds the ray at binned position wbase + j
-    uint32_t wbase = run_cur, wcnt = 0u, wtake = 0u;
-    float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0, s2 = s0;
-    uint4 s3 = make_uint4(0u, 0u, 0u, 0u), sm = s3;
-    auto load_window = [&]() {
-        if (run_cur >= run_end) {  // next run
+    auto next_window = [&](uint32_t &b, uint32_t &c) {
+        if (run_cur >= run_end) {
             run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt)));
             run_end = run_cur < n ? (run_cur + R < n ? run_cur + R : n) : run_cur;
             if (lane == 0 && run_cur < n) nxt = atomicAdd(&P.ctrl[1], R);
         }
-        wbase = run_cur;
-        wcnt = run_end - run_cur < 64u ? run_end - run_cur : 64u;
+        b = run_cur;
+        c = run_end - run_cur < 64u ? run_end - run_cur : 64u;
+        run_cur += c;
+    };
+    // next window: its slots, one per lane
+    uint32_t nb = 0u, nc = 0u, nslot = 0u;
+    next_window(nb, nc);
+    if (uint32_t(lane) < nc) nslot = P.idx[nb + uint32_t(lane)];
+    // staged window: lane j holds the ray of binned position wbase + j
+    uint32_t wbase = 0u, wcnt = 0u, wtake = 0u;
+    float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0, s2 = s0;
+    uint4 s3 = make_uint4(0u, 0u, 0u, 0u);
+    uint2 sh = make_uint2(0u, 0u);
+    auto stage = [&]() {
+        wbase = nb;
+        wcnt = nc;
         wtake = 0u;
-        run_cur += wcnt;
         if (uint32_t(lane) < wcnt) {
-            const uint4 *v = reinterpret_cast<const uint4 *>(P.rs + wbase + uint32_t(lane));
+            const uint4 *v = reinterpret_cast<const uint4 *>(P.rin + nslot);
             const uint4 a = v[0], b = v[1], c = v[2];
             s0 = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
             s1 = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w));
             s2 = make_float4(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w));
             s3 = v[3];
-            sm = P.mask_s[wbase + uint32_t(lane)];
+            if (P.wide) sh = P.mask_hi[nslot];
+        }
+        if (wcnt != 0u) {
+            next_window(nb, nc);
+            if (uint32_t(lane) < nc) nslot = P.idx[nb + uint32_t(lane)];
         }
     };
-    load_window();
+    stage();
 
     int state = ST_FREE;
     uint32_t rng = 0u, sid = 0u, pos = 0u;
@@ -335,9 +352,13 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                         b3 = __shfl(s1.w, src, 64);
             const float c0 = __shfl(s2.x, src, 64), c1 = __shfl(s2.y, src, 64), c2 = __shfl(s2.z, src, 64),
                         c3 = __shfl(s2.w, src, 64);
-            const uint32_t d0 = uint32_t(__shfl(int(s3.x), src, 64)), d1 = uint32_t(__shfl(int(s3.y), src, 64));
-            const uint32_t m0 = uint32_t(__shfl(int(sm.x), src, 64)), m1 = uint32_t(__shfl(int(sm.y), src, 64)),
-                           m2 = uint32_t(__shfl(int(sm.z), src, 64)), m3 = uint32_t(__shfl(int(sm.w), src, 64));
+            const uint32_t d0 = uint32_t(__shfl(int(s3.x), src, 64)), d1 = uint32_t(__shfl(int(s3.y), src, 64)),
+                           d2 = uint32_t(__shfl(int(s3.z), src, 64)), d3 = uint32_t(__shfl(int(s3.w), src, 64));
+            uint32_t e0 = 0u, e1 = 0u;
+            if (P.wide) {
+                e0 = uint32_t(__shfl(int(sh.x), src, 64));
+                e1 = uint32_t(__shfl(int(sh.y), src, 64));
+            }
             if (got) {
                 ro = pt_f3{a0, a1, a2};
                 rd = pt_f3{a3, b0, b1};
@@ -345,8 +366,8 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 ret = pt_f3{c1, c2, c3};
                 rng = d0;
                 sid = d1;
-                ck.lo = uint64_t(m0) | (uint64_t(m1) << 32);
-                ck.hi = uint64_t(m2) | (uint64_t(m3) << 32);
+                ck.lo = uint64_t(d2) | (uint64_t(d3) << 32);
+                ck.hi = uint64_t(e0) | (uint64_t(e1) << 32);
                 pos = wbase + uint32_t(src);
                 seg = P.bounce;
                 t = 0.0f;
@@ -354,7 +375,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 state = ST_MARCH;
             }
             wtake += take;
-            if (wtake == wcnt) load_window();  // wcnt = 0: no rays left for this wave
+            if (wtake == wcnt) stage();  // wcnt = 0: no rays left for this wave
         }
         const bool more = wcnt != 0u;
         tm = st.lap(PT_ST_CYC_REFILL, tm);
@@ -376,7 +397,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         }
         tm = st.lap(PT_ST_CYC_MAP, tm);
 
-        // ---- 3. shading (batched); ended paths store, the rest write back --
+        // ---- 3. shading (batched); ended paths store, the rest move on ----
         const uint64_t shadem = __ballot(state == ST_SHADE);
         if (shadem != 0ull &&
             (__popcll(shadem) >= shade_batch || __ballot(state == ST_MARCH || state == ST_NORMAL) == 0ull || !more)) {
@@ -386,9 +407,9 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 if (done) {
                     const pt_f3 c = final_color(L.debug, seg, L.bounces, ret);
                     P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
-                    reinterpret_cast<uint4 *>(P.ru + pos)[3] = make_uint4(rng, PT_BIN_NONE, 0u, 0u);
+                    P.rout[pos].sid = PT_BIN_NONE;
                 } else {
-                    store_ray(P.ru + pos, ro, rd, thr, ret, rng, sid);
+                    store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, 0u, 0u);
                 }
                 state = ST_FREE;
             }

@@ -64,9 +64,9 @@ struct pt_ctx {
     int bin_samples = -1;  // binned pipeline: samples per chunk; -1 = env (PT_BIN_SAMPLES), default 2^27
     PtJitModule jit_mod;   // loaded scene kernel (key = its source)
     // binned pipeline buffers (pt_binned.h), for bin_cap samples per chunk
-    PtRay *d_ray[2] = {nullptr, nullptr};  // unbinned, binned
-    uint4 *d_mask[2] = {nullptr, nullptr};
-    uint32_t *d_key = nullptr, *d_hist = nullptr, *d_offs = nullptr, *d_ctrl = nullptr;
+    PtRay *d_ray[2] = {nullptr, nullptr};  // ping-pong: pass k reads d_ray[k & 1], writes the other
+    uint2 *d_mask_hi = nullptr;            // check[] bits 64..127 (scenes with > 64 entries)
+    uint32_t *d_key = nullptr, *d_idx = nullptr, *d_hist = nullptr, *d_offs = nullptr, *d_ctrl = nullptr;
     float4 *d_color = nullptr;
     size_t bin_cap = 0, ctrl_words = 0;
     int cu_count = 0;
@@ -418,8 +418,8 @@ int pt_set_tiles(pt_ctx *c, uint32_t rank, uint32_t nranks) {
 }
 
 // ---- binned pipeline (pt_binned.h) -------------------------------------------
-// per sample of a chunk: rays and masks unbinned + binned, bin key, colour
-constexpr size_t kBinBytesPerSample = 2 * sizeof(PtRay) + 2 * sizeof(uint4) + sizeof(uint32_t) + sizeof(float4);
+// per sample of a chunk: two ray buffers, high mask words, bin key, binned slot, colour
+constexpr size_t kBinBytesPerSample = 2 * sizeof(PtRay) + sizeof(uint2) + 2 * sizeof(uint32_t) + sizeof(float4);
 
 static size_t bin_samples(const pt_ctx *c) {
     if (c->bin_samples > 0) return size_t(c->bin_samples);
@@ -433,16 +433,16 @@ static size_t bin_samples(const pt_ctx *c) {
 static void free_bin(pt_ctx *c) {
     (void)hipFree(c->d_ray[0]);
     (void)hipFree(c->d_ray[1]);
-    (void)hipFree(c->d_mask[0]);
-    (void)hipFree(c->d_mask[1]);
+    (void)hipFree(c->d_mask_hi);
     (void)hipFree(c->d_key);
+    (void)hipFree(c->d_idx);
     (void)hipFree(c->d_hist);
     (void)hipFree(c->d_offs);
     (void)hipFree(c->d_ctrl);
     (void)hipFree(c->d_color);
     c->d_ray[0] = c->d_ray[1] = nullptr;
-    c->d_mask[0] = c->d_mask[1] = nullptr;
-    c->d_key = c->d_hist = c->d_offs = c->d_ctrl = nullptr;
+    c->d_mask_hi = nullptr;
+    c->d_key = c->d_idx = c->d_hist = c->d_offs = c->d_ctrl = nullptr;
     c->d_color = nullptr;
     c->bin_cap = c->ctrl_words = 0;
 }
@@ -455,9 +455,9 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes) {
     free_bin(c);
     if (hipMalloc(&c->d_ray[0], samples * sizeof(PtRay)) != hipSuccess ||
         hipMalloc(&c->d_ray[1], samples * sizeof(PtRay)) != hipSuccess ||
-        hipMalloc(&c->d_mask[0], samples * sizeof(uint4)) != hipSuccess ||
-        hipMalloc(&c->d_mask[1], samples * sizeof(uint4)) != hipSuccess ||
+        hipMalloc(&c->d_mask_hi, samples * sizeof(uint2)) != hipSuccess ||
         hipMalloc(&c->d_key, samples * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_idx, samples * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_color, samples * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->d_hist, PT_BINS * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_offs, PT_BINS * sizeof(uint32_t)) != hipSuccess ||
@@ -466,7 +466,7 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes) {
         (void)hipGetLastError();
         return fail(c, PT_ERR_HIP, "out of device memory for the binned pipeline");
     }
-    HIPCHK(c, hipMemset(c->d_hist, 0, PT_BINS * sizeof(uint32_t)));
+    HIPCHK(c, hipMemsetAsync(c->d_hist, 0, PT_BINS * sizeof(uint32_t), c->stream));
     c->bin_cap = samples;
     c->ctrl_words = words;
     if (!c->cu_count) HIPCHK(c, hipDeviceGetAttribute(&c->cu_count, hipDeviceAttributeMultiprocessorCount, c->device));
@@ -522,11 +522,11 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         P.L.frame0 = int32_t(uint32_t(frame0) + done);
         P.L.last_clear0 = int32_t(uint32_t(lc0) + done);
         P.L.spp = int32_t(fr);
-        P.ru = c->d_ray[0];
-        P.rs = c->d_ray[1];
-        P.mask_u = c->d_mask[0];
-        P.mask_s = c->d_mask[1];
+        P.rin = c->d_ray[0];
+        P.rout = c->d_ray[1];
+        P.mask_hi = c->d_mask_hi;
         P.key = c->d_key;
+        P.idx = c->d_idx;
         P.hist = c->d_hist;
         P.offs = c->d_offs;
         P.color = c->d_color;
@@ -535,11 +535,14 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         P.n_src_const = uint32_t(n0);
         P.n_pix = int32_t(n_pix);
         P.frames = int32_t(fr);
+        P.wide = c->n_check > 64 ? 1 : 0;
         pt_launch_bin(PtBinStage::Gen, P, stats, item_grid(n0), c->stream);
         HIPCHK(c, hipGetLastError());
         for (int k = 0; k < passes; ++k) {
-            // pass k: bin the rays in ru (gen's, or those trace k-1 wrote back), trace them
+            // pass k: bin the rays of d_ray[k & 1] (gen's, or those trace k-1 wrote), trace them into the other
             P.bounce = k;
+            P.rin = c->d_ray[k & 1];
+            P.rout = c->d_ray[(k + 1) & 1];
             P.ctrl = c->d_ctrl + 4 * k;
             P.n_src = k == 0 ? nullptr : c->d_ctrl + 4 * (k - 1);
             if (k > 0) {

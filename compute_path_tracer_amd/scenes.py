@@ -207,6 +207,25 @@ def nested_demo() -> SDFEditor:
     return SDFEditor([outer, top2])
 
 
+def wide_graph(seed: int = 7, unions: int = 12, per_union: int = 8) -> SDFEditor:
+    """c3's room plus `unions` x `per_union` small random shapes, all with
+    AABBs: more than 64 check[] entries (exercises the high mask words)."""
+    rng = np.random.default_rng(seed)
+    ed = c3_graph32()
+    for ui in range(unions):
+        u = _union(f"cloud-{ui}", pos=(rng.uniform(-0.5, 0.5), rng.uniform(-0.3, 0.3), rng.uniform(0.0, 1.0)))
+        for k in range(per_union):
+            kind = Shapes.SPHERE if rng.random() < 0.6 else Shapes.CUBE
+            size = (rng.uniform(0.05, 0.2),) if kind == Shapes.SPHERE else tuple(rng.uniform(0.05, 0.2, 3))
+            s = _shape(kind, pos=(rng.uniform(-2.2, 2.2), rng.uniform(-1.0, 1.6), rng.uniform(0.0, 4.0)),
+                       rot=tuple(rng.uniform(-1.0, 1.0, 3)), size=size, name=f"cloud-{ui}-{k}")
+            _mat(s, col=tuple(rng.uniform(0.2, 0.9, 3)), brightness=2.0 if rng.random() < 0.1 else 0.0,
+                 spec=float(rng.choice([0.0, 0.5])), rough=0.3)
+            u.children_shapes.append(s)
+        ed.header_unions.append(u)
+    return ed
+
+
 def c3_no_aabb() -> SDFEditor:
     """c3 with every Transform.aabb off (profiling aid: no per-lane culling)."""
     ed = c3_graph32()
@@ -223,6 +242,7 @@ SCENES = {
     "c3": c3_graph32,
     "nested": nested_demo,
     "c3_noaabb": c3_no_aabb,
+    "wide": wide_graph,
 }
 
 # BASELINE.json configs -> (scene, width, height, spp, bounces)

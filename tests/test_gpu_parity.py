@@ -61,6 +61,7 @@ def _report(gpu, ref):
     ("c2", 96, 64, 4, 4),
     ("c3", 96, 54, 2, 8),
     ("nested", 64, 64, 3, 6),
+    ("wide", 48, 32, 2, 6),        # 124 check[] entries: the high mask words
 ])
 def test_parity_path_trace(gpu, name, w, h, spp, bounces, kernel):
     gpu_img, ref = _render_pair(scenes.SCENES[name](), w, h, spp, bounces, kernel=kernel)
@@ -137,7 +138,11 @@ def test_progressive_equals_batched(gpu):
     b.constants.last_clear -= 1
     b.render(5)
     ia, ib = a.read_image(), b.read_image()
-    assert np.array_equal(ia.view(np.uint32), ib.view(np.uint32))
+    ref = O.OracleScene(ed.rows()).render(48, 32, O.Constants(0.0, 1, float(np.float32(48) / np.float32(32)), 1),
+                                          O.Settings(0, 4, 1.0, 1.0, 0), 5)
+    bad_a = (ia.view(np.uint32) != ref.view(np.uint32)).any(-1)
+    bad_b = (ib.view(np.uint32) != ref.view(np.uint32)).any(-1)
+    assert not bad_a.any() and not bad_b.any(), (np.argwhere(bad_a)[:8].tolist(), np.argwhere(bad_b)[:8].tolist())
     assert a.constants.frame == b.constants.frame == 5
 
 
