@@ -59,6 +59,7 @@ struct PtPass {
     int32_t n_pix;          // local pixel slots: n_tiles * 64
     int32_t frames;         // frames in this chunk
     int32_t wide;           // check[] has more than 64 entries
+    int32_t run_max;        // trace: longest run of binned rays a wave takes at once (multiple of 64)
 };
 
 namespace pt {
@@ -276,22 +277,28 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     st.init();
     const uint64_t t_start = st.clk();
     const uint32_t n = P.ctrl[0];
-    // run length: about 8 runs per wave, 64..1024 rays, whole windows
+    // Run length: about 8 runs per wave, 64..run_max rays, whole windows.
+    // (Measured: fixed 256-ray runs beat both longer runs and guided sizes
+    // that shrink towards the end of the pass.)
+    const uint32_t rmax = uint32_t(P.run_max);
     uint32_t R = n / (gridDim.x * 8u);
-    R = R < 64u ? 64u : (R > 1024u ? 1024u : (R + 63u) & ~63u);
+    R = R < 64u ? 64u : (R > rmax ? rmax : (R + 63u) & ~63u);
+    auto run_len = [&](uint32_t) { return R; };
     const int shade_batch = L.shade_batch > 0 ? L.shade_batch : 1;
 
     // runs [run_cur, run_end); the next run is reserved one run ahead
-    uint32_t nxt = 0u;
-    if (lane == 0) nxt = atomicAdd(&P.ctrl[1], R);
+    uint32_t nxt = 0u, nxt_len = run_len(0u);
+    if (lane == 0) nxt = atomicAdd(&P.ctrl[1], nxt_len);
     uint32_t run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt))), run_end = 0u;
-    run_end = run_cur < n ? (run_cur + R < n ? run_cur + R : n) : run_cur;
-    if (lane == 0 && run_cur < n) nxt = atomicAdd(&P.ctrl[1], R);
+    run_end = run_cur < n ? (run_cur + nxt_len < n ? run_cur + nxt_len : n) : run_cur;
+    nxt_len = run_len(run_cur);
+    if (lane == 0 && run_cur < n) nxt = atomicAdd(&P.ctrl[1], nxt_len);
     auto next_window = [&](uint32_t &b, uint32_t &c) {
         if (run_cur >= run_end) {
             run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt)));
-            run_end = run_cur < n ? (run_cur + R < n ? run_cur + R : n) : run_cur;
-            if (lane == 0 && run_cur < n) nxt = atomicAdd(&P.ctrl[1], R);
+            run_end = run_cur < n ? (run_cur + nxt_len < n ? run_cur + nxt_len : n) : run_cur;
+            nxt_len = run_len(run_cur);
+            if (lane == 0 && run_cur < n) nxt = atomicAdd(&P.ctrl[1], nxt_len);
         }
         b = run_cur;
         c = run_end - run_cur < 64u ? run_end - run_cur : 64u;

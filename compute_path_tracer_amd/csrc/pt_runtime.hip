@@ -536,6 +536,12 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         P.n_pix = int32_t(n_pix);
         P.frames = int32_t(fr);
         P.wide = c->n_check > 64 ? 1 : 0;
+        static const int run_max = [] {  // A/B knob
+            const char *v = std::getenv("PT_BIN_RUN");
+            const int r = v ? std::atoi(v) : 256;
+            return r >= 64 ? (r / 64) * 64 : 256;
+        }();
+        P.run_max = run_max;
         pt_launch_bin(PtBinStage::Gen, P, stats, item_grid(n0), c->stream);
         HIPCHK(c, hipGetLastError());
         for (int k = 0; k < passes; ++k) {
@@ -628,9 +634,7 @@ static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, u
     }();
     L.kernel = c->kernel >= 0 ? c->kernel : env_kernel;
     if (L.kernel == PT_KERNEL_AUTO) L.kernel = PT_KERNEL_BINNED;
-    // measured defaults: binned 12, tile-resident wavefront 16
-    L.shade_batch = c->shade_batch > 0 ? c->shade_batch
-                                       : (env_batch > 0 ? env_batch : (L.kernel == PT_KERNEL_BINNED ? 12 : 16));
+    L.shade_batch = c->shade_batch > 0 ? c->shade_batch : (env_batch > 0 ? env_batch : 16);  // measured best
     return PT_OK;
 }
 
