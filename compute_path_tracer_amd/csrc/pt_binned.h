@@ -29,6 +29,7 @@
 #define PT_BIN_BITS 12
 #define PT_BINS (1 << PT_BIN_BITS)
 #define PT_BIN_NONE 0xffffffffu
+#define PT_BIN_LIVE 0xfffffffeu  // trace -> bounds: a ray was written at this position
 #define PT_BIN_BLOCK 256  // threads per block of the gen / bounds / scatter kernels
 #define PT_SCATTER_ITEMS 16
 
@@ -38,7 +39,7 @@ struct PtRay {  // a path between two segments, 64 B
     float thr[3];
     float ret[3];
     uint32_t rng;
-    uint32_t sid;      // sample slot: frame * n_pix + local pixel; PT_BIN_NONE: path ended
+    uint32_t sid;      // sample slot: frame * n_pix + local pixel
     uint32_t mask[2];  // check[] bits 0..63 of the segment (bits 64..127: PtPass.mask_hi)
 };
 
@@ -47,7 +48,7 @@ struct PtPass {
     PtRay *rin;             // this pass's rays, by slot (gen / bounds: the rays being binned)
     PtRay *rout;            // trace: next pass's rays, by binned position
     uint2 *mask_hi;         // check[] bits 64..127 per rin slot (scenes with > 64 entries)
-    uint32_t *key;          // bin per rin slot (PT_BIN_NONE: no live ray)
+    uint32_t *key;          // bin per rin slot (PT_BIN_NONE: no live ray); trace writes NONE / LIVE per rout position
     uint32_t *idx;          // rin slots in bin order
     uint32_t *hist;         // [PT_BINS] counts, zero outside gen/bounds -> scan
     uint32_t *offs;         // [PT_BINS] scatter cursors
@@ -155,9 +156,10 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
     flush_stats<ST>(L, st);
 }
 
-// bounds: mask + bin of every ray the last trace pass wrote.  Each wave
-// compacts the live rays of its slots through an LDS queue, so ended paths
-// (their slots hold only the end marker) leave no lane idle.
+// bounds: mask + bin of every ray the last trace pass wrote.  The trace
+// marked each position LIVE or NONE in key[]; each wave compacts the live
+// positions of its slots through an LDS queue, so ended paths cost neither a
+// record read nor an idle lane.
 template <bool ST>
 __device__ __forceinline__ void bin_bounds_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
@@ -183,11 +185,7 @@ __device__ __forceinline__ void bin_bounds_body(const PtPass &P) {
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + uint32_t(wv)) * 64u; base < n; base += waves * 64u) {
         const uint32_t i = base + uint32_t(lane);
-        bool live = false;
-        if (i < n) {
-            live = P.rin[i].sid != PT_BIN_NONE;
-            if (!live) P.key[i] = PT_BIN_NONE;
-        }
+        const bool live = i < n && P.key[i] == PT_BIN_LIVE;
         const uint64_t lm = __ballot(live);
         if (live) q[qn + uint32_t(lane_rank(lm))] = i;
         qn += uint32_t(__popcll(lm));
@@ -414,9 +412,10 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 if (done) {
                     const pt_f3 c = final_color(L.debug, seg, L.bounces, ret);
                     P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
-                    P.rout[pos].sid = PT_BIN_NONE;
+                    P.key[pos] = PT_BIN_NONE;
                 } else {
                     store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, 0u, 0u);
+                    P.key[pos] = PT_BIN_LIVE;
                 }
                 state = ST_FREE;
             }
