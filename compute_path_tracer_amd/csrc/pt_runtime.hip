@@ -646,8 +646,11 @@ int pt_dispatch(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     c->tev_used = 0;
     if (spp > 0 && L.n_tiles > 0) {
-        // bound a single launch's length; chunks continue frame/last_clear
-        const uint32_t chunk = 64;
+        // bound a single launch's length; chunks continue frame/last_clear.
+        // The binned pipeline takes every frame at once: it splits by its own
+        // sample budget, and larger chunks mean fuller passes (at N GPUs each
+        // rank owns 1/N of the pixels and renders N times the frames).
+        const uint32_t chunk = use_binned(L) ? spp : 64;
         for (uint32_t done = 0; done < spp; done += chunk) {
             PtLaunch Lc = L;
             Lc.spp = int32_t(std::min(chunk, spp - done));
