@@ -90,20 +90,22 @@ PT_HD void pt_sincos(float x, float &s, float &c) {
     }
 }
 
-// Correctly rounded f32 sqrt.  Same result as the compiler's IEEE sqrtf
-// lowering (v_sqrt_f32 + the two-neighbour FMA correction): for inputs below
-// 2^-96 (where that lowering rescales) the wave takes the full sqrtf; zeros,
-// +inf and NaN fall out of the correction unchanged.  Verified against sqrtf
-// for all 2^32 inputs by pt_selftest / tests/test_gpu_selftest.py.
+// Correctly rounded f32 sqrt: g = x*rsq(x) and one residual correction
+// g + (x - g*g) * rsq(x)/2 (exact residual by fma) for x in [2^-96, 2^128);
+// the rest (zeros, negatives, tiny, inf, NaN) takes the wave through the
+// IEEE sqrtf.  Verified equal to sqrtf for all 2^32 inputs by pt_selftest /
+// tests/test_gpu_selftest.py.
 PT_HD float pt_sqrt(float x) {
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
-    if (__builtin_expect(__ballot(x < 0x1p-96f) != 0ull, 0)) return sqrtf(x);
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float sd = __int_as_float(__float_as_int(s) - 1);
-    const float su = __int_as_float(__float_as_int(s) + 1);
-    float r = fmaf(-sd, s, x) <= 0.0f ? sd : s;
-    r = fmaf(-su, s, x) > 0.0f ? su : r;
-    return r;
+    // x in [2^-96, 2^128) as an unsigned range test on the bits; anything else
+    // (zeros, negatives, tiny, inf, NaN) takes the IEEE sqrtf for the wave
+    if (__builtin_expect(__ballot((__float_as_uint(x) - 0x0F800000u) >= (0x7F800000u - 0x0F800000u)) != 0ull, 0))
+        return sqrtf(x);
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float g = x * y;
+    const float h = 0.5f * y;
+    const float r = fmaf(-g, g, x);
+    return fmaf(r, h, g);
 #else
     return sqrtf(x);
 #endif
