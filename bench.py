@@ -295,6 +295,15 @@ def main() -> None:
     }
     if validation is not None:
         out["validation"] = validation
+    # display pass, outside the timed region: HBM-bound
+    # elementwise kernel, 16 B read + 4 B written per pixel (sRGB8 surface)
+    pt.display(srgb8=True)
+    dms = [pt.get_option("display_ms") for _ in range(3) if pt.display(srgb8=True) is not None]
+    d_ms = float(min(dms))
+    d_bytes = 20.0 * args.width * args.height
+    out["display"] = {"kernel": "pt_display_kernel (srgb8)", "ms": round(d_ms, 4),
+                      "achieved_gbs": round(d_bytes / (d_ms * 1e-3) / 1e9, 1), "peak_gbs": PEAK_HBM_GBS,
+                      "algorithmic_bytes": d_bytes}
     tr_prof = profiled_traffic(out["config"])
     if tr_prof is not None:
         out["roofline"]["traffic"] = tr_prof[0]

@@ -27,6 +27,7 @@ PT_OP_UNION_BEGIN, PT_OP_SHAPE, PT_OP_UNION_END = 0, 1, 2
 PT_COMBINE_ASSIGN, PT_COMBINE_UNION, PT_COMBINE_SUBTRACTION = 0, 1, 2
 PT_SO_SCALAR, PT_SO_VEC3, PT_SO_ONE, PT_SO_TORUS = 0, 1, 2, 3
 PT_COMM_ID_BYTES = 128
+PT_DISPLAY_RGBA32F, PT_DISPLAY_SRGB8 = 0, 1
 PT_STAT_COUNT = 32
 STAT_NAMES = (
     "samples", "segments", "march_steps", "normal_maps", "shaded", "aabb_tests", "xform_union", "xform_shape",
@@ -43,7 +44,7 @@ SYMBOLS = (
     "pt_comm_init", "pt_reduce_accum", "pt_read_reduced", "pt_sync", "pt_last_dispatch_ms",
     "pt_dispatch_stats", "pt_set_option", "pt_get_option", "pt_jit_log", "pt_jit_compile", "pt_last_error",
     "pt_destroy", "pt_abi_version", "pt_device_math", "pt_check_sqrt_exhaustive", "pt_check_div_exhaustive",
-    "pt_check_div_random",
+    "pt_check_div_random", "pt_display", "pt_write_accum",
 )
 PT_MATH = {"max": 0, "min": 1, "sqrt": 2, "sqrtf": 3, "sin": 4, "cos": 5, "div": 6, "fma": 7}
 
@@ -139,6 +140,8 @@ def lib() -> ctypes.CDLL:
         "pt_check_div_exhaustive": (c_int, [c_int, c_uint32, c_uint32, c_uint32, c_uint32, POINTER(c_uint64),
                                             POINTER(c_uint64)]),
         "pt_check_div_random": (c_int, [c_int, c_uint32, c_uint32, POINTER(c_uint64), POINTER(c_uint64)]),
+        "pt_display": (c_int, [c_void_p, c_int, c_void_p, c_size_t]),
+        "pt_write_accum": (c_int, [c_void_p, POINTER(c_float), c_size_t]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -144,3 +144,80 @@ PT_HD pt_f3 pt_normalize(pt_f3 a) {
     float l = pt_length(a);
     return pt_f3{a.x / l, a.y / l, a.z / l};
 }
+
+// ---- display contract (render_texture_shader.wgsl) ------------------------
+// WGSL pow's precision is the driver's (parity unpinned there).  Contract:
+// pow(x, y) for x > 0 evaluated in double with fixed series and explicit
+// fma (log2 via 2*atanh on [sqrt(1/2), sqrt(2)), exp2 via Taylor on
+// [-1/2, 1/2]), rounded once to f32 -- identical on host and device and
+// within one f32 ulp of the true value.  x == 0 gives 0.
+PT_HD double pt_log2_d(double x) {
+    int e = 0;
+    double m = frexp(x, &e);  // x = m * 2^e, m in [0.5, 1)
+    m *= 2.0;
+    e -= 1;
+    if (m > 1.4142135623730951) {
+        m *= 0.5;
+        e += 1;
+    }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double p = 1.0 / 23.0;
+    p = fma(p, s2, 1.0 / 21.0);
+    p = fma(p, s2, 1.0 / 19.0);
+    p = fma(p, s2, 1.0 / 17.0);
+    p = fma(p, s2, 1.0 / 15.0);
+    p = fma(p, s2, 1.0 / 13.0);
+    p = fma(p, s2, 1.0 / 11.0);
+    p = fma(p, s2, 1.0 / 9.0);
+    p = fma(p, s2, 1.0 / 7.0);
+    p = fma(p, s2, 1.0 / 5.0);
+    p = fma(p, s2, 1.0 / 3.0);
+    p = fma(p, s2, 1.0);
+    const double ln_m = (2.0 * s) * p;
+    return double(e) + ln_m * 1.4426950408889634;  // 1 / ln 2
+}
+PT_HD double pt_exp2_d(double t) {  // |t| < 1000
+    const double k = floor(t + 0.5), z = (t - k) * 0.6931471805599453;
+    double p = 1.0 / 6227020800.0;  // 1/13!
+    p = fma(p, z, 1.0 / 479001600.0);
+    p = fma(p, z, 1.0 / 39916800.0);
+    p = fma(p, z, 1.0 / 3628800.0);
+    p = fma(p, z, 1.0 / 362880.0);
+    p = fma(p, z, 1.0 / 40320.0);
+    p = fma(p, z, 1.0 / 5040.0);
+    p = fma(p, z, 1.0 / 720.0);
+    p = fma(p, z, 1.0 / 120.0);
+    p = fma(p, z, 1.0 / 24.0);
+    p = fma(p, z, 1.0 / 6.0);
+    p = fma(p, z, 0.5);
+    p = fma(p, z, 1.0);
+    p = fma(p, z, 1.0);
+    return ldexp(p, int(k));
+}
+PT_HD float pt_pow_pos(float x, float y) {
+    if (!(x > 0.0f)) return 0.0f;
+    return float(pt_exp2_d(double(y) * pt_log2_d(double(x))));
+}
+// LinearToSRGB (render_texture_shader.wgsl:31-38): clamp, pow(1/2.4) branch,
+// linear branch, mix by LessThan.  The constant 1/2.4 is WGSL abstract-float
+// arithmetic rounded to f32.
+PT_HD float pt_linear_to_srgb(float v) {
+    const float c = pt_gmin(pt_gmax(v, 0.0f), 1.0f);
+    const float a = pt_pow_pos(c, float(1.0 / 2.4)) * 1.055f - 0.055f;
+    const float b = c * 12.92f;
+    const float t = c < 0.0031308f ? 1.0f : 0.0f;
+    return a * (1.0f - t) + b * t;
+}
+// ACESFilm (render_texture_shader.wgsl:49-56)
+PT_HD float pt_aces(float x) {
+    const float n = x * (2.51f * x + 0.03f), d = x * (2.43f * x + 0.59f) + 0.14f;
+    return pt_gmin(pt_gmax(n / d, 0.0f), 1.0f);
+}
+// color_corection + fs_main's output (:62-72, :81-94): exposure 1, ACES, sRGB
+PT_HD float pt_display_channel(float x) { return pt_linear_to_srgb(pt_aces(x * 1.0f)); }
+// The sRGB swapchain (setup.rs:53-59 picks an sRGB format) encodes the
+// fragment output once more and stores 8 bits (round to nearest even).
+PT_HD uint32_t pt_srgb8(float fs_out) {
+    const float s = pt_linear_to_srgb(fs_out);
+    return uint32_t(rintf(s * 255.0f));
+}

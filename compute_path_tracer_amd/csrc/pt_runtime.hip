@@ -74,6 +74,11 @@ struct pt_ctx {
     // HIP events around each trace-pass launch of the last dispatch (pairs)
     std::vector<hipEvent_t> tev;
     size_t tev_used = 0;
+    // display pass output (device) and its timing
+    void *d_display = nullptr;
+    size_t cap_display = 0;
+    hipEvent_t dev0 = nullptr, dev1 = nullptr;
+    bool display_timed = false;
     std::string jit_log;
     double jit_seconds = 0.0;
     std::string err;
@@ -695,6 +700,38 @@ int pt_read_accum(pt_ctx *c, float *rgba, size_t bytes) {
     return PT_OK;
 }
 
+int pt_write_accum(pt_ctx *c, const float *rgba, size_t bytes) {
+    if (!c) return PT_ERR_INVALID;
+    const size_t need = size_t(c->width) * c->height * 16;
+    if (!rgba || bytes < need) return fail(c, PT_ERR_SIZE, "image buffer too small");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (need) HIPCHK(c, hipMemcpyAsync(c->accum, rgba, need, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_display(pt_ctx *c, int format, void *out, size_t bytes) {
+    if (!c) return PT_ERR_INVALID;
+    if (format != PT_DISPLAY_RGBA32F && format != PT_DISPLAY_SRGB8) return fail(c, PT_ERR_INVALID, "bad display format");
+    const size_t need = size_t(c->width) * c->height * (format == PT_DISPLAY_RGBA32F ? 16 : 4);
+    if (!out || bytes < need) return fail(c, PT_ERR_SIZE, "display buffer too small");
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = ensure(c, &c->d_display, c->cap_display, std::max<size_t>(need, 16));
+    if (rc != PT_OK) return rc;
+    if (!c->dev0) {
+        HIPCHK(c, hipEventCreate(&c->dev0));
+        HIPCHK(c, hipEventCreate(&c->dev1));
+    }
+    HIPCHK(c, hipEventRecord(c->dev0, c->stream));
+    pt_launch_display(c->accum, c->width, c->height, format, c->d_display, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->dev1, c->stream));
+    c->display_timed = true;
+    if (need) HIPCHK(c, hipMemcpyAsync(out, c->d_display, need, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
 int pt_accum_device_ptr(pt_ctx *c, void **dev_ptr, size_t *bytes) {
     if (!c || !dev_ptr || !bytes) return PT_ERR_INVALID;
     *dev_ptr = c->accum;
@@ -811,6 +848,11 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "shade_batch")) *value = c->shade_batch;
     else if (!std::strcmp(key, "bin_samples")) *value = double(bin_samples(c));
     else if (!std::strcmp(key, "trace_launches")) *value = double(c->tev_used / 2);
+    else if (!std::strcmp(key, "display_ms")) {
+        float ms = 0.0f;
+        if (c->display_timed) HIPCHK(c, hipEventElapsedTime(&ms, c->dev0, c->dev1));
+        *value = ms;
+    }
     else if (!std::strcmp(key, "trace_ms")) {  // summed device time of the last dispatch's trace passes
         double sum = 0.0;
         if (c->tev_used) HIPCHK(c, hipEventSynchronize(c->tev[c->tev_used - 1]));
@@ -846,6 +888,9 @@ void pt_destroy(pt_ctx *c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
+    (void)hipFree(c->d_display);
+    if (c->dev0) (void)hipEventDestroy(c->dev0);
+    if (c->dev1) (void)hipEventDestroy(c->dev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

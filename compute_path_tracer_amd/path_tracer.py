@@ -165,6 +165,26 @@ class PathTracer:
                                                           out.nbytes))
         return out
 
+    def write_image(self, img: np.ndarray) -> None:
+        """Replace the accumulation image (pt_write_accum): float32 [h][w][4]."""
+        w, h = self.size
+        a = np.ascontiguousarray(img, np.float32)
+        if a.shape != (h, w, 4):
+            raise ValueError(f"image must be ({h}, {w}, 4), got {a.shape}")
+        self._chk("pt_write_accum", self._L.pt_write_accum(self._ctx, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                                            a.nbytes))
+
+    def display(self, srgb8: bool = False) -> np.ndarray:
+        """The display pass (RenderTexturePipeline::render_pass,
+        render_texture_shader.wgsl:23-94) on the device.  srgb8=False: fs_main's
+        RGBA32F per texel [height][width][4], row 0 = bottom.  srgb8=True: the
+        sRGB swapchain's 8-bit RGBA [height][width][4], row 0 = top of screen."""
+        w, h = self.size
+        out = np.empty((h, w, 4), dtype=np.uint8 if srgb8 else np.float32)
+        fmt = N.PT_DISPLAY_SRGB8 if srgb8 else N.PT_DISPLAY_RGBA32F
+        self._chk("pt_display", self._L.pt_display(self._ctx, fmt, out.ctypes.data_as(ctypes.c_void_p), out.nbytes))
+        return out
+
     # -- RCCL ------------------------------------------------------------
     @staticmethod
     def comm_unique_id() -> bytes:

@@ -155,6 +155,10 @@ int pt_dispatch(pt_ctx *ctx, const pt_constants *c, const pt_settings *s, uint32
 /* == State::save_image readback (state.rs:237-303): blocking copy of the
  * local image (w*h*4 floats) into a caller buffer. */
 int pt_read_accum(pt_ctx *ctx, float *rgba, size_t bytes);
+/* Inverse of pt_read_accum (new): replace the local image with w*h*4 floats
+ * from a caller buffer (resume a progressive render from a saved image, or
+ * feed the display pass).  Blocking. */
+int pt_write_accum(pt_ctx *ctx, const float *rgba, size_t bytes);
 /* Device pointer + size of the local image (for external collectives). */
 int pt_accum_device_ptr(pt_ctx *ctx, void **dev_ptr, size_t *bytes);
 int pt_get_size(const pt_ctx *ctx, uint32_t *width, uint32_t *height);
@@ -178,6 +182,18 @@ int pt_last_dispatch_ms(pt_ctx *ctx, float *ms);
 #define PT_STAT_COUNT 32
 int pt_dispatch_stats(pt_ctx *ctx, const pt_constants *c, const pt_settings *s, uint32_t spp,
                       uint64_t counters[PT_STAT_COUNT]);
+/* Display pass (replaces RenderTexturePipeline::render_pass,
+ * render_texture_pipeline.rs:77-110 + render_texture_shader.wgsl:23-94):
+ * ACESFilm + LinearToSRGB of the accumulation image.
+ *   PT_DISPLAY_RGBA32F: fs_main's vec4 per texel, texel order (row 0 =
+ *     bottom), w*h*16 bytes;
+ *   PT_DISPLAY_SRGB8: the 8-bit RGBA the sRGB swapchain (setup.rs:53-59)
+ *     stores -- encoded a second time, the reference's double-sRGB -- in
+ *     screen order (row 0 = top), w*h*4 bytes.
+ * Blocking; the output buffer is caller-owned (host memory). */
+#define PT_DISPLAY_RGBA32F 0
+#define PT_DISPLAY_SRGB8 1
+int pt_display(pt_ctx *ctx, int format, void *out, size_t bytes);
 /* Tuning knobs: "kernel" (0 auto = 3, 1 simple one-path-per-lane, 2 tile-
  * resident wavefront state machine, 3 mask-binned passes: per bounce, the
  * rays of a chunk of frames are grouped by their bounds() check set before
@@ -193,7 +209,8 @@ int pt_set_option(pt_ctx *ctx, const char *key, int value);
  * "jit_seconds" (last hipRTC compile time), "kernel", "shade_batch",
  * "bin_samples", "bin_bytes" (device memory held by the binned pipeline),
  * "trace_ms" / "trace_launches" (device time and count of the last dispatch's
- * binned trace passes, HIP events on the context stream). */
+ * binned trace passes, HIP events on the context stream), "display_ms"
+ * (device time of the last pt_display's kernel). */
 int pt_get_option(pt_ctx *ctx, const char *key, double *value);
 /* Log of the last failed scene-kernel build ("" if none). */
 const char *pt_jit_log(const pt_ctx *ctx);

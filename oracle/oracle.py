@@ -11,7 +11,7 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
-from ctypes import POINTER, Structure, c_float, c_int, c_int32, c_uint8, c_uint32, c_uint64
+from ctypes import POINTER, Structure, c_float, c_int, c_int32, c_uint8, c_uint32, c_uint64, c_void_p
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -78,6 +78,10 @@ def lib():
         L.pto_bounds.argtypes = [vp, POINTER(c_float), POINTER(c_float), POINTER(c_uint8), POINTER(c_float)]
         L.pto_render.argtypes = [vp, POINTER(c_float), c_int, c_int, POINTER(Constants), POINTER(Settings), c_int,
                                  c_int, c_int, c_int, c_int, POINTER(Counters)]
+        L.pto_display.argtypes = [POINTER(c_float), c_int, c_int, c_int, vp]
+        L.pto_display.restype = None
+        L.pto_pow_pos.argtypes = [c_float, c_float]
+        L.pto_pow_pos.restype = c_float
         _lib = L
     return _lib
 
@@ -185,3 +189,17 @@ def sin(x: float) -> float:
 
 def cos(x: float) -> float:
     return float(lib().pto_cos(x))
+
+
+def display(image: np.ndarray, srgb8: bool = False) -> np.ndarray:
+    """The display pass restated (pto_display): fs_main RGBA32F per texel, or
+    the sRGB swapchain's 8-bit RGBA in screen order."""
+    img = np.ascontiguousarray(image, np.float32)
+    h, w = img.shape[:2]
+    out = np.empty((h, w, 4), np.uint8 if srgb8 else np.float32)
+    lib().pto_display(img.ctypes.data_as(POINTER(c_float)), w, h, 1 if srgb8 else 0, out.ctypes.data_as(c_void_p))
+    return out
+
+
+def pow_pos(x: float, y: float) -> float:
+    return float(lib().pto_pow_pos(x, y))

@@ -719,3 +719,80 @@ void pto_render(const pto_scene *s, float *image, int w, int h, const pto_consta
     free(jobs);
     free(th);
 }
+
+/* ---- display pass (render_texture_shader.wgsl:23-94) --------------------- */
+/* pow(x, y), x > 0: log2 by frexp + 2*atanh series on [sqrt(1/2), sqrt(2)),
+ * exp2 by rounding off the integer part + Taylor series of e^(f ln 2),
+ * all in double with fma, rounded once to f32 (DESIGN.md display contract). */
+static double d_log2(double x)
+{
+    int e = 0;
+    double m = frexp(x, &e) * 2.0, s, s2, p;
+    static const double inv_odd[12] = {1.0 / 23.0, 1.0 / 21.0, 1.0 / 19.0, 1.0 / 17.0, 1.0 / 15.0, 1.0 / 13.0,
+                                       1.0 / 11.0, 1.0 / 9.0,  1.0 / 7.0,  1.0 / 5.0,  1.0 / 3.0,  1.0};
+    e -= 1;
+    if (m > 1.4142135623730951) {
+        m *= 0.5;
+        e += 1;
+    }
+    s = (m - 1.0) / (m + 1.0);
+    s2 = s * s;
+    p = inv_odd[0];
+    for (int k = 1; k < 12; ++k) p = fma(p, s2, inv_odd[k]);
+    return (double)e + ((2.0 * s) * p) * 1.4426950408889634;
+}
+
+static double d_exp2(double t)
+{
+    static const double inv_fact[14] = {1.0 / 6227020800.0, 1.0 / 479001600.0, 1.0 / 39916800.0, 1.0 / 3628800.0,
+                                        1.0 / 362880.0,     1.0 / 40320.0,     1.0 / 5040.0,     1.0 / 720.0,
+                                        1.0 / 120.0,        1.0 / 24.0,        1.0 / 6.0,        0.5,
+                                        1.0,                1.0};
+    const double k = floor(t + 0.5), z = (t - k) * 0.6931471805599453;
+    double p = inv_fact[0];
+    for (int i = 1; i < 14; ++i) p = fma(p, z, inv_fact[i]);
+    return ldexp(p, (int)k);
+}
+
+float pto_pow_pos(float x, float y)
+{
+    if (!(x > 0.0f)) return 0.0f;
+    return (float)d_exp2((double)y * d_log2((double)x));
+}
+
+static float lin_to_srgb(float v)
+{
+    const float c = gclamp(v, 0.0f, 1.0f);
+    const float a = pto_pow_pos(c, (float)(1.0 / 2.4)) * 1.055f - 0.055f;
+    const float b = c * 12.92f;
+    const float t = c < 0.0031308f ? 1.0f : 0.0f;
+    return a * (1.0f - t) + b * t;
+}
+
+static float aces(float x)
+{
+    const float n = x * (2.51f * x + 0.03f), d = x * (2.43f * x + 0.59f) + 0.14f;
+    return gclamp(n / d, 0.0f, 1.0f);
+}
+
+static float fs_channel(float x) { return lin_to_srgb(aces(x * 1.0f)); }
+
+void pto_display(const float *image, int w, int h, int fmt, void *out)
+{
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            if (fmt == 0) {
+                const float *t = image + ((size_t)y * w + x) * 4;
+                float *o = (float *)out + ((size_t)y * w + x) * 4;
+                o[0] = fs_channel(t[0]);
+                o[1] = fs_channel(t[1]);
+                o[2] = fs_channel(t[2]);
+                o[3] = 1.0f;
+            } else {
+                const float *t = image + ((size_t)(h - 1 - y) * w + x) * 4;
+                uint8_t *o = (uint8_t *)out + ((size_t)y * w + x) * 4;
+                for (int k = 0; k < 3; ++k) o[k] = (uint8_t)rintf(lin_to_srgb(fs_channel(t[k])) * 255.0f);
+                o[3] = 255;
+            }
+        }
+}

@@ -113,6 +113,14 @@ void pto_render(const pto_scene *s, float *image, int w, int h,
                 int rank, int nranks, int row_stride, int nthreads,
                 pto_counters *counters);
 
+/* Display pass, render_texture_shader.wgsl:23-94 (+ the sRGB swapchain,
+ * setup.rs:53-59), under DESIGN.md's display contract: pow in double with
+ * fixed series and fma, rounded once to f32.  fmt 0: fs_main's RGBA32F per
+ * texel (texel order); fmt 1: 8-bit RGBA as the sRGB surface stores it,
+ * screen order (row 0 = top = texel row h-1). */
+void pto_display(const float *image, int w, int h, int fmt, void *out);
+float pto_pow_pos(float x, float y);
+
 /* Analysis aid: log every path segment (ray, check mask, march steps) of
  * subsequent single-threaded renders into buf (counters must be requested). */
 typedef struct { float ro[3], rd[3]; uint64_t mask[2]; int32_t seg, steps, hit, pad; } pto_segment;
