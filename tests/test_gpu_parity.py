@@ -221,3 +221,28 @@ def test_work_counters_match_oracle(gpu, kernel):
               "xform_shape", "sdf_sphere", "sdf_cube", "sdf_octahedron", "comb_union", "comb_sub", "comb_assign",
               "rr_break"):
         assert got[k] == ct[k], (k, got[k], ct[k])
+
+
+@pytest.mark.parametrize("name,spp", [("c3", 16), ("c2", 16)])
+def test_full_size_tiles_match_oracle(gpu, name, spp):
+    """BASELINE configs at full resolution: 8 random 8x8 tiles, plus every tile
+    holding a non-finite texel (normalize of a zero vector upstream), against
+    the oracle rendering just that tile (rank = tile, nranks = #tiles)."""
+    scene, w, h, _, bounces = scenes.CONFIGS[name]
+    ed = scenes.SCENES[scene]()
+    st = N.Settings(debug=0, bounces=bounces, scale=1.0, fov=1.0, aabb=0)
+    pt = PathTracer(w, h, ed.compile(CompData()), settings=st)
+    aspect = float(np.float32(w) / np.float32(h))
+    pt.dispatch(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), spp)
+    img = pt.read_image()
+    pt.close()
+    tx, ntiles = (w + 7) // 8, ((w + 7) // 8) * ((h + 7) // 8)
+    bad = {(int(y) // 8) * tx + int(x) // 8 for y, x in np.argwhere(~np.isfinite(img[..., :3]).all(-1))}
+    tiles = sorted(set(np.random.default_rng(11).choice(ntiles, 8, replace=False).tolist()) | bad)
+    osc = O.OracleScene(ed.rows())
+    for t in tiles:
+        ref = osc.render(w, h, O.Constants(0.0, 1, aspect, 1), O.Settings(0, bounces, 1.0, 1.0, 0), spp, rank=t,
+                         nranks=ntiles, threads=8)
+        y0, x0 = (t // tx) * 8, (t % tx) * 8
+        a, b = img[y0:y0 + 8, x0:x0 + 8], ref[y0:y0 + 8, x0:x0 + 8]
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), t
