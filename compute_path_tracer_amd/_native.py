@@ -103,9 +103,10 @@ def lib() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"HIP library {LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
-    L = ctypes.CDLL(LIB_PATH)
+    path = os.environ.get("PT_LIB") or LIB_PATH  # PT_LIB: an in-tree A/B variant (build.build_variant)
+    if not os.path.exists(path):
+        raise ImportError(f"HIP library {path} missing: run __graft_entry__.build() (no CPU fallback exists)")
+    L = ctypes.CDLL(path)
     ctx = c_void_p
     u32p = POINTER(c_uint32)
     sig = {
