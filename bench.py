@@ -170,6 +170,9 @@ def main() -> None:
     prog = ed.compile(CompData())
     settings = N.Settings(debug=0, bounces=args.bounces, scale=1.0, fov=1.0, aabb=0)
     pt = PathTracer(args.width, args.height, prog, device=local_rank, settings=settings)
+    # setup, untimed: install the values-baked scene kernel (jit_bake 2 tier-up;
+    # an interactive caller keeps rendering on the table kernel meanwhile)
+    pt.set_option("jit_wait", 1)
     aspect = float(np.float32(args.width) / np.float32(args.height))
     spp_step = args.spp * world  # weak scaling: each rank owns 1/world of the tiles
     tr = TileSplitRender(pt, rank, world, aspect, reduce="rccl" if args.dist_backend == "nccl" else "host")
@@ -291,7 +294,9 @@ def main() -> None:
                 "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "algorithmic_bytes_per_launch": bytes_per_launch},
         "work": st,
         "schedule": schedule_metrics(st),
-        "jit": {"active": jit, "compile_s": round(pt.get_option("jit_seconds"), 3)},
+        "jit": {"active": jit, "compile_s": round(pt.get_option("jit_seconds"), 3),
+                "tier_active": bool(pt.get_option("jit_tier_active")),
+                "tier_compile_s": round(pt.get_option("jit_tier_seconds"), 3)},
     }
     if validation is not None:
         out["validation"] = validation

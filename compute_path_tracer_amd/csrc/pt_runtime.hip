@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <future>
 #include <map>
 #include <mutex>
 #include <cstdio>
@@ -60,9 +61,18 @@ struct pt_ctx {
     int kernel = -1;       // PT_KERNEL_*; -1 = environment / auto
     int shade_batch = -1;  // -1 = environment / default
     int jit = -1;          // 1 use per-scene hipRTC kernels, 0 interpreter; -1 = env (PT_JIT), default 1
-    int jit_bake = -1;     // 1 bake node values as literals; -1 = env (PT_JIT_BAKE), default 0
+    int jit_bake = -1;     // 0 values from the node table, 1 baked as literals, 2 tier-up; -1 = env (PT_JIT_BAKE), default 2
     int bin_samples = -1;  // binned pipeline: samples per chunk; -1 = env (PT_BIN_SAMPLES), default 2^27
-    PtJitModule jit_mod;   // loaded scene kernel (key = its source)
+    PtJitModule jit_mod;   // scene kernel for the topology (key = its source)
+    // tier-up (jit_bake 2): the same kernel with the current values baked in as
+    // literals, compiled on a worker thread and used once ready while the
+    // values stay unchanged -- value edits never wait for a compile
+    PtJitModule jit_tier;
+    std::string tier_want;  // baked source for the current values
+    std::string tier_job_src;
+    std::string tier_failed;  // a baked source that did not build (not retried)
+    std::future<std::vector<char>> tier_job;  // code object (empty: compile failed)
+    double tier_seconds = 0.0;
     // binned pipeline buffers (pt_binned.h), for bin_cap samples per chunk
     PtRay *d_ray[2] = {nullptr, nullptr};  // ping-pong: pass k reads d_ray[k & 1], writes the other
     uint2 *d_mask_hi = nullptr;            // check[] bits 64..127 (scenes with > 64 entries)
@@ -96,13 +106,71 @@ std::mutex &jit_mutex() {
     return m;
 }
 
-bool jit_bake(const pt_ctx *c) {
-    if (c->jit_bake >= 0) return c->jit_bake != 0;
+int jit_bake(const pt_ctx *c) {
+    if (c->jit_bake >= 0) return c->jit_bake;
     static const int env = [] {
         const char *v = std::getenv("PT_JIT_BAKE");
-        return v ? std::atoi(v) : 0;
+        const int b = v ? std::atoi(v) : 2;
+        return (b >= 0 && b <= 2) ? b : 2;
     }();
-    return env != 0;
+    return env;
+}
+
+// Code object for a generated source: from the process-wide cache, else
+// compiled (without holding the cache lock).  Empty on failure (log set).
+std::vector<char> jit_code(const std::string &src, std::string &log, double *seconds) {
+    {
+        std::lock_guard<std::mutex> g(jit_mutex());
+        auto it = jit_cache().find(src);
+        if (it != jit_cache().end()) return it->second;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<char> code;
+    if (!pt_jit_compile_source(src, code, log)) code.clear();
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!code.empty()) {
+        std::lock_guard<std::mutex> g(jit_mutex());
+        jit_cache()[src] = code;
+    }
+    return code;
+}
+
+// Install a finished tier-up compile if it is still the one the current
+// values want; start the wanted one if nothing is pending.  wait: block on a
+// pending compile first.
+void jit_tier_poll(pt_ctx *c, bool wait) {
+    if (c->tier_job.valid() &&
+        (wait || c->tier_job.wait_for(std::chrono::seconds(0)) == std::future_status::ready)) {
+        std::vector<char> code = c->tier_job.get();
+        if (code.empty()) c->tier_failed = c->tier_job_src;
+        if (!code.empty() && c->tier_job_src == c->tier_want && !c->jit_tier.module) {
+            std::string err;
+            if (pt_jit_load(code, c->jit_tier, err)) {
+                c->jit_tier.key = c->tier_job_src;
+            } else {
+                c->jit_log = err;
+                c->tier_failed = c->tier_job_src;
+            }
+        }
+        c->tier_job_src.clear();
+    }
+    if (!c->tier_job.valid() && !c->tier_want.empty() && c->jit_tier.key != c->tier_want &&
+        c->tier_want != c->tier_failed) {
+        std::string src = c->tier_want;
+        c->tier_job_src = src;
+        double *secs = &c->tier_seconds;
+        c->tier_job = std::async(std::launch::async, [src, secs]() {
+            std::string log;
+            return jit_code(src, log, secs);
+        });
+        if (wait) jit_tier_poll(c, true);
+    }
+}
+
+// The scene kernel in use: the tier-up build when loaded, else the topology one.
+const PtJitModule *jit_active(const pt_ctx *c) {
+    if (c->jit_tier.module) return &c->jit_tier;
+    return c->jit_mod.module ? &c->jit_mod : nullptr;
 }
 
 bool jit_wanted(const pt_ctx *c) {
@@ -119,36 +187,32 @@ bool jit_wanted(const pt_ctx *c) {
 void jit_refresh(pt_ctx *c, const std::vector<PtNode> &nodes) {
     if (!jit_wanted(c)) {
         pt_jit_unload(c->jit_mod);
+        pt_jit_unload(c->jit_tier);
+        c->tier_want.clear();
         return;
     }
-    std::string src = pt_jit_source(nodes, jit_bake(c));
-    if (c->jit_mod.module && c->jit_mod.key == src) return;
-    pt_jit_unload(c->jit_mod);
-    std::vector<char> code;
-    {
-        std::lock_guard<std::mutex> g(jit_mutex());
-        auto it = jit_cache().find(src);
-        if (it != jit_cache().end()) {
-            code = it->second;
-        } else {
-            const auto t0 = std::chrono::steady_clock::now();
-            std::string log;
-            const bool ok = pt_jit_compile_source(src, code, log);
-            c->jit_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            if (!ok) {
-                c->jit_log = "hipRTC compile failed: " + log;
-                return;
-            }
-            jit_cache()[src] = code;
+    const int bake = jit_bake(c);
+    std::string src = pt_jit_source(nodes, bake == 1);
+    // the tier-up build for these values (jit_bake 2); a stale one is dropped
+    c->tier_want = bake == 2 ? pt_jit_source(nodes, true) : std::string();
+    if (c->jit_tier.module && c->jit_tier.key != c->tier_want) pt_jit_unload(c->jit_tier);
+    if (!(c->jit_mod.module && c->jit_mod.key == src)) {
+        pt_jit_unload(c->jit_mod);
+        std::string log;
+        std::vector<char> code = jit_code(src, log, &c->jit_seconds);
+        if (code.empty()) {
+            c->jit_log = "hipRTC compile failed: " + log;
+            return;
         }
+        std::string err;
+        if (!pt_jit_load(code, c->jit_mod, err)) {
+            c->jit_log = err;
+            return;
+        }
+        c->jit_mod.key = std::move(src);
+        c->jit_log.clear();
     }
-    std::string err;
-    if (!pt_jit_load(code, c->jit_mod, err)) {
-        c->jit_log = err;
-        return;
-    }
-    c->jit_mod.key = std::move(src);
-    c->jit_log.clear();
+    if (bake == 2) jit_tier_poll(c, false);
 }
 
 int fail(pt_ctx *c, int code, const std::string &msg) {
@@ -511,8 +575,9 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         const size_t tile = PT_BIN_BLOCK * PT_SCATTER_ITEMS;
         return unsigned(std::max<size_t>(1, std::min<size_t>((n + tile - 1) / tile, 4 * cu)));
     };
-    const bool jit = c->jit_mod.module != nullptr;
-    hipFunction_t jf = jit ? (stats ? c->jit_mod.trace_stats : c->jit_mod.trace) : nullptr;
+    const PtJitModule *jm = jit_active(c);
+    const bool jit = jm != nullptr;
+    hipFunction_t jf = jit ? (stats ? jm->trace_stats : jm->trace) : nullptr;
     int per_cu = 0;
     if (jit) HIPCHK(c, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jf, 64, 0));
     else per_cu = pt_bin_trace_blocks_per_cu(stats);
@@ -585,9 +650,10 @@ static bool use_binned(const PtLaunch &L) { return L.kernel == PT_KERNEL_BINNED 
 // the ahead-of-time kernels (pt_kernel.hip).
 static int launch(pt_ctx *c, PtLaunch &L, bool stats) {
     if (use_binned(L)) return launch_binned(c, L, stats);
-    if (!pt_use_simple_kernel(L) && c->jit_mod.module) {
+    const PtJitModule *jm = jit_active(c);
+    if (!pt_use_simple_kernel(L) && jm) {
         void *args[] = {&L};
-        HIPCHK(c, hipModuleLaunchKernel(stats ? c->jit_mod.render_stats : c->jit_mod.render, unsigned(L.n_tiles), 1, 1,
+        HIPCHK(c, hipModuleLaunchKernel(stats ? jm->render_stats : jm->render, unsigned(L.n_tiles), 1, 1,
                                         64, 1, 1, 0, c->stream, args, nullptr));
     } else {
         pt_launch_render(L, stats, c->stream);
@@ -648,6 +714,7 @@ int pt_dispatch(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t
     int rc = make_launch(c, k, s, spp, L);
     if (rc != PT_OK) return rc;
     HIPCHK(c, hipSetDevice(c->device));
+    jit_tier_poll(c, false);  // switch to the values-baked kernel once it is built
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     c->tev_used = 0;
     if (spp > 0 && L.n_tiles > 0) {
@@ -819,12 +886,21 @@ int pt_set_option(pt_ctx *c, const char *key, int value) {
     if (!std::strcmp(key, "jit")) {
         if (value != 0 && value != 1) return fail(c, PT_ERR_INVALID, "jit must be 0 or 1");
         c->jit = value;
-        if (!value) pt_jit_unload(c->jit_mod);  // re-enabled on the next pt_set_data
+        if (!value) {  // re-enabled on the next pt_set_data
+            pt_jit_unload(c->jit_mod);
+            pt_jit_unload(c->jit_tier);
+            c->tier_want.clear();
+        }
         return PT_OK;
     }
     if (!std::strcmp(key, "jit_bake")) {
-        if (value != 0 && value != 1) return fail(c, PT_ERR_INVALID, "jit_bake must be 0 or 1");
+        if (value < 0 || value > 2) return fail(c, PT_ERR_INVALID, "jit_bake must be 0, 1 or 2");
         c->jit_bake = value;  // takes effect at the next pt_set_data
+        return PT_OK;
+    }
+    if (!std::strcmp(key, "jit_wait")) {  // block until a pending tier-up build is installed
+        HIPCHK(c, hipSetDevice(c->device));
+        jit_tier_poll(c, true);
         return PT_OK;
     }
     if (!std::strcmp(key, "bin_samples")) {
@@ -842,7 +918,9 @@ int pt_set_option(pt_ctx *c, const char *key, int value) {
 
 int pt_get_option(pt_ctx *c, const char *key, double *value) {
     if (!c || !key || !value) return PT_ERR_INVALID;
-    if (!std::strcmp(key, "jit_active")) *value = c->jit_mod.module ? 1.0 : 0.0;
+    if (!std::strcmp(key, "jit_active")) *value = jit_active(c) ? 1.0 : 0.0;
+    else if (!std::strcmp(key, "jit_tier_active")) *value = c->jit_tier.module ? 1.0 : 0.0;
+    else if (!std::strcmp(key, "jit_tier_seconds")) *value = c->tier_seconds;
     else if (!std::strcmp(key, "jit_seconds")) *value = c->jit_seconds;
     else if (!std::strcmp(key, "kernel")) *value = c->kernel;
     else if (!std::strcmp(key, "shade_batch")) *value = c->shade_batch;
@@ -877,7 +955,9 @@ void pt_destroy(pt_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->tier_job.valid()) c->tier_job.wait();
     pt_jit_unload(c->jit_mod);
+    pt_jit_unload(c->jit_tier);
     (void)hipFree(c->accum);
     (void)hipFree(c->reduced);
     (void)hipFree(c->d_nodes);

@@ -199,14 +199,20 @@ int pt_display(pt_ctx *ctx, int format, void *out, size_t bytes);
  * rays of a chunk of frames are grouped by their bounds() check set before
  * they are marched), "shade_batch" (state-machine kernels: lanes that must
  * wait before a shading pass runs, 1..64), "bin_samples" (binned kernel:
- * samples per chunk, >= 64; device memory = 160 B per sample) and "jit" (1:
+ * samples per chunk, >= 64; device memory = 160 B per sample), "jit" (1:
  * per-scene hipRTC build of the state-machine kernels, compiled at
  * pt_set_data when the topology or an identity flag changed -- the analogue
- * of remake_pipeline; 0: op-list interpreter).  Results are bit-identical for
- * every value. */
+ * of remake_pipeline; 0: op-list interpreter), "jit_bake" (0: node values
+ * read from the table; 1: baked into the kernel as literals, recompiled on
+ * every value edit; 2, the default: tier-up -- the table kernel runs at
+ * once, and a values-baked build compiled on a worker thread replaces it
+ * while the values stay unchanged) and "jit_wait" (block until a pending
+ * tier-up build is installed).  Results are bit-identical for every value. */
 int pt_set_option(pt_ctx *ctx, const char *key, int value);
 /* Read back: "jit_active" (1 when the scene-specialised kernel is loaded),
- * "jit_seconds" (last hipRTC compile time), "kernel", "shade_batch",
+ * "jit_seconds" (last hipRTC compile time), "jit_tier_active" /
+ * "jit_tier_seconds" (values-baked build in use / its compile time),
+ * "kernel", "shade_batch",
  * "bin_samples", "bin_bytes" (device memory held by the binned pipeline),
  * "trace_ms" / "trace_launches" (device time and count of the last dispatch's
  * binned trace passes, HIP events on the context stream), "display_ms"

@@ -20,9 +20,18 @@ RMS_TOL = 1e-5
 
 
 KERNELS = {"simple": {"kernel": "simple", "jit": 0}, "wave": {"kernel": "wave", "jit": 0},
-           "jit": {"kernel": "wave", "jit": 1}, "binned": {"kernel": "binned", "jit": 0},
-           "binned_jit": {"kernel": "binned", "jit": 1}}
-ALL = ["simple", "wave", "jit", "binned", "binned_jit"]
+           "jit": {"kernel": "wave", "jit": 1, "jit_bake": 0}, "binned": {"kernel": "binned", "jit": 0},
+           "binned_jit": {"kernel": "binned", "jit": 1, "jit_bake": 0},
+           "binned_bake": {"kernel": "binned", "jit": 1, "jit_bake": 1},
+           "binned_tier": {"kernel": "binned", "jit": 1, "jit_bake": 2}}
+ALL = ["simple", "wave", "jit", "binned", "binned_jit", "binned_bake", "binned_tier"]
+
+
+def _tier_up(pt, opts):
+    """jit_bake 2: wait for the values-baked build, so the test runs on it."""
+    if opts.get("jit_bake") == 2:
+        pt.set_option("jit_wait", 1)
+        assert pt.get_option("jit_tier_active") == 1.0, pt.jit_log()
 
 
 def _render_pair(ed, w, h, spp, bounces, debug=0, frame=1, last_clear=1, fov=1.0, aspect=None, kernel="jit",
@@ -37,6 +46,7 @@ def _render_pair(ed, w, h, spp, bounces, debug=0, frame=1, last_clear=1, fov=1.0
     pt = PathTracer(w, h, prog, settings=st, options=opts)
     if opts["jit"]:
         assert pt.get_option("jit_active") == 1.0, pt.jit_log()
+    _tier_up(pt, opts)
     a = float(np.float32(w) / np.float32(h)) if aspect is None else aspect
     pt.dispatch(N.Constants(time=0.0, frame=frame, aspect=a, last_clear=last_clear), spp)
     gpu = pt.read_image()
@@ -213,6 +223,7 @@ def test_work_counters_match_oracle(gpu, kernel):
     prog = ed.compile(CompData())
     st = N.Settings(debug=0, bounces=8, scale=1.0, fov=1.0, aabb=0)
     pt = PathTracer(64, 40, prog, settings=st, options=KERNELS[kernel])
+    _tier_up(pt, KERNELS[kernel])
     a = float(np.float32(64) / np.float32(40))
     got = pt.stats(N.Constants(time=0.0, frame=1, aspect=a, last_clear=1), 2)
     _, ct = O.OracleScene(ed.rows()).render(64, 40, O.Constants(0.0, 1, a, 1), O.Settings(0, 8, 1.0, 1.0, 0), 2,
@@ -246,3 +257,37 @@ def test_full_size_tiles_match_oracle(gpu, name, spp):
         y0, x0 = (t // tx) * 8, (t % tx) * 8
         a, b = img[y0:y0 + 8, x0:x0 + 8], ref[y0:y0 + 8, x0:x0 + 8]
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), t
+
+
+def test_jit_tier_up_follows_value_edits(gpu):
+    """jit_bake 2: the table kernel serves at once; the values-baked build
+    takes over after jit_wait; a value edit drops it (stale literals) until
+    the rebuilt one is waited for.  Every image stays exact."""
+    ed = scenes.c2_sphere_box_torus()
+    cd = CompData()
+    prog = ed.compile(cd)
+    st = N.Settings(debug=0, bounces=3, scale=1.0, fov=1.0, aabb=0)
+    pt = PathTracer(40, 30, prog, settings=st, options={"kernel": "binned", "jit": 1, "jit_bake": 2})
+    c = N.Constants(time=0.0, frame=1, aspect=float(np.float32(40) / np.float32(30)), last_clear=1)
+
+    def check():
+        pt.clear()
+        pt.dispatch(c, 2)
+        ref = O.OracleScene(ed.rows()).render(40, 30, O.Constants(0.0, 1, c.aspect, 1), O.Settings(0, 3, 1.0, 1.0, 0),
+                                              2)
+        assert np.array_equal(pt.read_image().view(np.uint32), ref.view(np.uint32))
+
+    check()
+    pt.set_option("jit_wait", 1)
+    assert pt.get_option("jit_tier_active") == 1.0  # (jit_tier_seconds is 0 on a process-cache hit)
+    check()
+    sph = ed.header_unions[0].children_shapes[1]
+    sph.transform.position.x.set(-0.25)  # value only: the baked build is stale
+    ed.data_update(cd)
+    pt.set_data(cd.data_array.as_array())
+    assert pt.get_option("jit_tier_active") == 0.0
+    check()
+    pt.set_option("jit_wait", 1)
+    assert pt.get_option("jit_tier_active") == 1.0
+    check()
+    pt.close()
