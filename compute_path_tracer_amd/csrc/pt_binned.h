@@ -32,9 +32,6 @@
 #define PT_BIN_LIVE 0xfffffffeu  // trace -> bounds: a ray was written at this position
 #define PT_BIN_BLOCK 256  // threads per block of the gen / bounds / scatter kernels
 #define PT_SCATTER_ITEMS 16
-#ifndef PT_BOUNDS_UNROLL
-#define PT_BOUNDS_UNROLL 4  // box loop unroll: scalar box loads issued ahead of their slab tests
-#endif
 
 struct PtRay {  // a path between two segments, 64 B
     float ro[3];
@@ -85,7 +82,7 @@ __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro,
                       pt_div_coord_ok(ro.z) && pt_div_dir_ok(rd.x) && pt_div_dir_ok(rd.y) && pt_div_dir_ok(rd.z);
     if (fast) {
         const float yx = 1.0f / rd.x, yy = 1.0f / rd.y, yz = 1.0f / rd.z;
-#pragma unroll PT_BOUNDS_UNROLL
+#pragma unroll 4  // scalar box loads issued ahead of their slab tests
         for (int b = 0; b < L.n_aabb; ++b) {
             const PtAabb bx = boxes[b];
             if (ray_box_rcp(bx, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, yx, yy, yz)) w[bx.back >> 5] |= 1u << (bx.back & 31);
