@@ -22,6 +22,7 @@ for name in names:
     prog = scenes.SCENES[scene]().compile(CompData())
     st = N.Settings(debug=0, bounces=bounces, scale=1.0, fov=1.0, aabb=0)
     pt = PathTracer(w, h, prog, settings=st)
+    pt.set_option("jit_wait", 1)  # setup: the values-baked scene kernel, as bench.py
     aspect = float(np.float32(w) / np.float32(h))
     pt.dispatch(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), min(spp, 4))  # warm-up
     pt.sync()
