@@ -29,7 +29,7 @@
 #define PT_BIN_BITS 12
 #define PT_BINS (1 << PT_BIN_BITS)
 #define PT_BIN_NONE 0xffffffffu
-#define PT_BIN_LIVE 0xfffffffeu  // trace -> bounds: a ray was written at this position
+#define PT_BIN_HIT 0xfffffffeu  // trace -> shade: a hit record was written at this position
 #define PT_BIN_BLOCK 256  // threads per block of the gen / bounds / scatter kernels
 #define PT_SCATTER_ITEMS 16
 
@@ -40,7 +40,8 @@ struct PtRay {  // a path between two segments, 64 B
     float ret[3];
     uint32_t rng;
     uint32_t sid;      // sample slot: frame * n_pix + local pixel
-    uint32_t mask[2];  // check[] bits 0..63 of the segment (bits 64..127: PtPass.mask_hi)
+    uint32_t mask[2];  // ray: check[] bits 0..63 of the segment (64..127: PtPass.mask_hi)
+                       // hit: [0] material index (normal differences in PtPass.hitn)
 };
 
 struct PtPass {
@@ -48,19 +49,21 @@ struct PtPass {
     PtRay *rin;             // this pass's rays, by slot (gen / bounds: the rays being binned)
     PtRay *rout;            // trace: next pass's rays, by binned position
     uint2 *mask_hi;         // check[] bits 64..127 per rin slot (scenes with > 64 entries)
-    uint32_t *key;          // bin per rin slot (PT_BIN_NONE: no live ray); trace writes NONE / LIVE per rout position
+    uint32_t *key;          // bin per rin slot (PT_BIN_NONE: no live ray); trace marks its rout positions NONE / HIT
     uint32_t *idx;          // rin slots in bin order
     uint32_t *hist;         // [PT_BINS] counts, zero outside gen/bounds -> scan
     uint32_t *offs;         // [PT_BINS] scatter cursors
     uint32_t *ctrl;         // this pass: [0] binned rays, [1] trace run cursor
     const uint32_t *n_src;  // rin slots (bounds / scatter), null: n_src_const
     float4 *color;          // [frames][n_pix] sample colours
+    float4 *hitn;           // trace -> shade: calc_normal's differences per rout position
     uint32_t n_src_const;
     int32_t bounce;         // segment index of this pass (path_trace's loop counter i)
     int32_t n_pix;          // local pixel slots: n_tiles * 64
     int32_t frames;         // frames in this chunk
     int32_t wide;           // check[] has more than 64 entries
     int32_t run_max;        // trace: longest run of binned rays a wave takes at once (multiple of 64)
+    int32_t refill_min;     // trace: refill when at least this many lanes are free (or none map)
 };
 
 namespace pt {
@@ -157,12 +160,15 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
     flush_stats<ST>(L, st);
 }
 
-// bounds: mask + bin of every ray the last trace pass wrote.  The trace
-// marked each position LIVE or NONE in key[]; each wave compacts the live
-// positions of its slots through an LDS queue, so ended paths cost neither a
-// record read nor an idle lane.
+// shade: every hit the last trace pass wrote (positions marked HIT) is
+// shaded -- material, new direction, emission, throughput, Russian roulette
+// (pt_path.h shade_lane, the same f32 steps and rng draws) -- and a path that
+// goes on gets its next segment's bounds() mask and bin.  Shading is taken
+// out of the trace pass, where it ran on a fraction of the lanes of a wave;
+// here, one thread per hit, it fills the VALU time this memory-latency-bound
+// pass had idle.  Each wave compacts its hit positions through an LDS queue.
 template <bool ST>
-__device__ __forceinline__ void bin_bounds_body(const PtPass &P) {
+__device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
     __shared__ uint32_t queue[PT_BIN_BLOCK / 64][128];
     hist_zero(lh);
@@ -175,9 +181,21 @@ __device__ __forceinline__ void bin_bounds_body(const PtPass &P) {
     uint32_t qn = 0u;  // wave-uniform queue length
     auto work = [&](uint32_t i) {
         const float4 *v = reinterpret_cast<const float4 *>(P.rin + i);
-        const float4 a = v[0], b = v[1];
-        const uint4 m = bounds_mask<ST>(L, pt_f3{a.x, a.y, a.z}, pt_f3{a.w, b.x, b.y}, st);
-        reinterpret_cast<uint2 *>(P.rin + i)[7] = make_uint2(m.x, m.y);
+        const float4 a = v[0], b = v[1], c = v[2];
+        const uint4 d = reinterpret_cast<const uint4 *>(P.rin + i)[3];
+        const float4 nd = P.hitn[i];
+        pt_f3 ro{a.x, a.y, a.z}, rd{a.w, b.x, b.y}, thr{b.z, b.w, c.x}, ret{c.y, c.z, c.w};
+        uint32_t rng = d.x;
+        int seg = P.bounce;
+        const bool done = shade_lane<ST>(L.mats, L.bounces, int(d.z), nd.x, nd.y, nd.z, 0, rng, ro, rd, thr, ret, seg, st);
+        if (done) {
+            const pt_f3 col = final_color(L.debug, seg, L.bounces, ret);
+            P.color[d.y] = make_float4(col.x, col.y, col.z, 0.0f);
+            P.key[i] = PT_BIN_NONE;
+            return;
+        }
+        const uint4 m = bounds_mask<ST>(L, ro, rd, st);
+        store_ray(P.rin + i, ro, rd, thr, ret, rng, d.y, m.x, m.y);
         if (P.wide) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);
         P.key[i] = k;
@@ -186,7 +204,7 @@ __device__ __forceinline__ void bin_bounds_body(const PtPass &P) {
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + uint32_t(wv)) * 64u; base < n; base += waves * 64u) {
         const uint32_t i = base + uint32_t(lane);
-        const bool live = i < n && P.key[i] == PT_BIN_LIVE;
+        const bool live = i < n && P.key[i] == PT_BIN_HIT;
         const uint64_t lm = __ballot(live);
         if (live) q[qn + uint32_t(lane_rank(lm))] = i;
         qn += uint32_t(__popcll(lm));
@@ -283,7 +301,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     uint32_t R = n / (gridDim.x * 8u);
     R = R < 64u ? 64u : (R > rmax ? rmax : (R + 63u) & ~63u);
     auto run_len = [&](uint32_t) { return R; };
-    const int shade_batch = L.shade_batch > 0 ? L.shade_batch : 1;
 
     // runs [run_cur, run_end); the next run is reserved one run ahead
     uint32_t nxt = 0u, nxt_len = run_len(0u);
@@ -345,7 +362,8 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         uint64_t tm = st.clk();
         // ---- 1. refill free lanes from the staging window --------------
         const uint64_t freem = __ballot(state == ST_FREE);
-        if (freem != 0ull && wcnt != 0u) {
+        if (freem != 0ull && wcnt != 0u &&
+            (__popcll(freem) >= P.refill_min || __ballot(state == ST_MARCH || state == ST_NORMAL) == 0ull)) {
             const uint32_t avail = wcnt - wtake, nf = uint32_t(__popcll(freem));
             const uint32_t take = nf < avail ? nf : avail;
             const int r = lane_rank(freem);
@@ -403,23 +421,19 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         }
         tm = st.lap(PT_ST_CYC_MAP, tm);
 
-        // ---- 3. shading (batched); ended paths store, the rest move on ----
-        const uint64_t shadem = __ballot(state == ST_SHADE);
-        if (shadem != 0ull &&
-            (__popcll(shadem) >= shade_batch || __ballot(state == ST_MARCH || state == ST_NORMAL) == 0ull || !more)) {
-            if (state == ST_SHADE) {
-                const bool done =
-                    shade_lane<ST>(L.mats, L.bounces, mat, dv0, dv1, dv2, step, rng, ro, rd, thr, ret, seg, st);
-                if (done) {
-                    const pt_f3 c = final_color(L.debug, seg, L.bounces, ret);
-                    P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
-                    P.key[pos] = PT_BIN_NONE;
-                } else {
-                    store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, 0u, 0u);
-                    P.key[pos] = PT_BIN_LIVE;
-                }
-                state = ST_FREE;
+        // ---- 3. hand finished segments on: a miss ends the path (its colour
+        // is final), a hit goes to the shade pass with its normal differences
+        if (state == ST_SHADE) {
+            if (step < 0) {
+                const pt_f3 c = final_color(L.debug, seg, L.bounces, ret);
+                P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
+                P.key[pos] = PT_BIN_NONE;
+            } else {
+                store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, uint32_t(mat), 0u);
+                P.hitn[pos] = make_float4(dv0, dv1, dv2, 0.0f);
+                P.key[pos] = PT_BIN_HIT;
             }
+            state = ST_FREE;
         }
         tm = st.lap(PT_ST_CYC_SHADE, tm);
         if (!more && __ballot(state != ST_FREE) == 0ull) break;

@@ -12,7 +12,7 @@
 // ahead-of-time kernels (pt_kernel.hip)
 bool pt_use_simple_kernel(const PtLaunch &L);
 void pt_launch_render(const PtLaunch &L, bool stats, hipStream_t stream);
-enum class PtBinStage { Gen, Bounds, Scan, Scatter, Trace, Fold };
+enum class PtBinStage { Gen, Shade, Scan, Scatter, Trace, Fold };
 void pt_launch_bin(PtBinStage stage, const PtPass &P, bool stats, unsigned grid, hipStream_t stream);
 int pt_bin_trace_blocks_per_cu(bool stats);  // occupancy of the interpreter trace kernel
 void pt_launch_display(const float *img, uint32_t w, uint32_t h, int fmt, void *out, hipStream_t stream);

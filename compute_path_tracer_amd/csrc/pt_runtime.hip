@@ -78,6 +78,7 @@ struct pt_ctx {
     uint2 *d_mask_hi = nullptr;            // check[] bits 64..127 (scenes with > 64 entries)
     uint32_t *d_key = nullptr, *d_idx = nullptr, *d_hist = nullptr, *d_offs = nullptr, *d_ctrl = nullptr;
     float4 *d_color = nullptr;
+    float4 *d_hitn = nullptr;  // trace -> shade: normal differences per position
     size_t bin_cap = 0, ctrl_words = 0;
     int cu_count = 0;
     bool fast_bounds = false;  // every box coordinate inside the reciprocal-division guard
@@ -487,8 +488,9 @@ int pt_set_tiles(pt_ctx *c, uint32_t rank, uint32_t nranks) {
 }
 
 // ---- binned pipeline (pt_binned.h) -------------------------------------------
-// per sample of a chunk: two ray buffers, high mask words, bin key, binned slot, colour
-constexpr size_t kBinBytesPerSample = 2 * sizeof(PtRay) + sizeof(uint2) + 2 * sizeof(uint32_t) + sizeof(float4);
+// per sample of a chunk: two ray buffers, high mask words, bin key, binned slot, colour, hit normal
+constexpr size_t kBinBytesPerSample =
+    2 * sizeof(PtRay) + sizeof(uint2) + 2 * sizeof(uint32_t) + sizeof(float4) + sizeof(float4);
 
 static size_t bin_samples(const pt_ctx *c) {
     if (c->bin_samples > 0) return size_t(c->bin_samples);
@@ -509,10 +511,12 @@ static void free_bin(pt_ctx *c) {
     (void)hipFree(c->d_offs);
     (void)hipFree(c->d_ctrl);
     (void)hipFree(c->d_color);
+    (void)hipFree(c->d_hitn);
     c->d_ray[0] = c->d_ray[1] = nullptr;
     c->d_mask_hi = nullptr;
     c->d_key = c->d_idx = c->d_hist = c->d_offs = c->d_ctrl = nullptr;
     c->d_color = nullptr;
+    c->d_hitn = nullptr;
     c->bin_cap = c->ctrl_words = 0;
 }
 
@@ -528,6 +532,7 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes) {
         hipMalloc(&c->d_key, samples * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_idx, samples * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_color, samples * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->d_hitn, samples * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->d_hist, PT_BINS * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_offs, PT_BINS * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_ctrl, words * sizeof(uint32_t)) != hipSuccess) {
@@ -600,6 +605,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         P.hist = c->d_hist;
         P.offs = c->d_offs;
         P.color = c->d_color;
+        P.hitn = c->d_hitn;
         P.ctrl = c->d_ctrl;
         P.n_src = nullptr;
         P.n_src_const = uint32_t(n0);
@@ -612,19 +618,39 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             return r >= 64 ? (r / 64) * 64 : 256;
         }();
         P.run_max = run_max;
+        static const int refill_min = [] {  // A/B knob
+            const char *v = std::getenv("PT_REFILL_MIN");
+            const int r = v ? std::atoi(v) : 4;
+            return r >= 1 && r <= 64 ? r : 4;
+        }();
+        P.refill_min = refill_min;
         pt_launch_bin(PtBinStage::Gen, P, stats, item_grid(n0), c->stream);
         HIPCHK(c, hipGetLastError());
+        // shade the hits trace pass k wrote into d_ray[(k + 1) & 1]: ended paths
+        // store their colour, the rest get their next ray, bounds() and bin
+        auto shade = [&](int k) -> int {
+            PtPass S = P;
+            S.bounce = k;
+            S.rin = c->d_ray[(k + 1) & 1];
+            S.n_src = c->d_ctrl + 4 * k;
+            static const unsigned shade_cu = [] {  // A/B knob: shade blocks per CU
+                const char *v = std::getenv("PT_SHADE_BLOCKS");
+                return v ? unsigned(std::atoi(v)) : 8u;
+            }();
+            const unsigned sg = unsigned(std::max<size_t>(1, std::min<size_t>((c->bin_cap + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK,
+                                                                            size_t(shade_cu) * cu)));
+            pt_launch_bin(PtBinStage::Shade, S, stats, sg, c->stream);
+            HIPCHK(c, hipGetLastError());
+            return PT_OK;
+        };
         for (int k = 0; k < passes; ++k) {
-            // pass k: bin the rays of d_ray[k & 1] (gen's, or those trace k-1 wrote), trace them into the other
+            // pass k: bin the rays of d_ray[k & 1] (gen's, or the shaded hits of pass k-1), trace them into the other
+            if (k > 0 && (rc = shade(k - 1)) != PT_OK) return rc;
             P.bounce = k;
             P.rin = c->d_ray[k & 1];
             P.rout = c->d_ray[(k + 1) & 1];
             P.ctrl = c->d_ctrl + 4 * k;
             P.n_src = k == 0 ? nullptr : c->d_ctrl + 4 * (k - 1);
-            if (k > 0) {
-                pt_launch_bin(PtBinStage::Bounds, P, stats, item_grid(c->bin_cap), c->stream);
-                HIPCHK(c, hipGetLastError());
-            }
             pt_launch_bin(PtBinStage::Scan, P, stats, 1, c->stream);
             pt_launch_bin(PtBinStage::Scatter, P, stats, scatter_grid(k == 0 ? n0 : c->bin_cap), c->stream);
             HIPCHK(c, hipGetLastError());
@@ -638,6 +664,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             }
             if (!stats) HIPCHK(c, record_trace_event(c));
         }
+        if ((rc = shade(passes - 1)) != PT_OK) return rc;  // the last bounce's hits end their paths
         pt_launch_bin(PtBinStage::Fold, P, stats, unsigned((n_pix + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK), c->stream);
         HIPCHK(c, hipGetLastError());
     }
