@@ -226,6 +226,45 @@ def wide_graph(seed: int = 7, unions: int = 12, per_union: int = 8) -> SDFEditor
     return ed
 
 
+_DEPRECATED_KINDS = {"Sphere": Shapes.SPHERE, "Cube": Shapes.CUBE, "OctahedronExact": Shapes.OCTAHEDRON}
+
+
+def deprecated_map(nodes) -> SDFEditor:
+    """A map saved by the reference's deprecated node editor
+    (assets/maps/*.json: a list of serde `Node`s,
+    assets/depricated/node_editor_package.rs:204-218 + its `Material`) as
+    a current editor scene.  One header union holds the nodes in file order.
+    Each node keeps its shape (OctahedronExact -> Octahedron), scale, size,
+    position and rotation.  Material fields are copied one for one
+    (light_strength -> Brightness).  A light colour of (0, 0, 0) becomes
+    the live editor's default (1, 1, 1): the current Mat normalises the
+    light colour, and zero would make every hit NaN.  AABB culling is on,
+    with the editor's default exaggeration.  `nodes`: the parsed JSON list,
+    or a path to the file."""
+    if isinstance(nodes, str):
+        import json
+
+        with open(nodes) as f:
+            nodes = json.load(f)
+    u = _union("map")
+    for n in nodes:
+        kind = _DEPRECATED_KINDS[n["shape"]]
+        m = n["material"]
+        light = tuple(m["light"])
+        s = _shape(kind, pos=tuple(n["position"]), rot=tuple(n["rotation"]), scale=n["scale"],
+                   size=tuple(n["size"]), name=n["title"])
+        _mat(s, col=tuple(m["color"]), brightness=m["light_strength"],
+             light=light if any(v != 0.0 for v in light) else (1.0, 1.0, 1.0), spec=m["spec"],
+             spec_col=tuple(m["spec_col"]), rough=m["roughness"])
+        mat = s.material
+        mat.ior.set(m["ior"])
+        mat.refract_chance.set(m["refraction_chance"])
+        mat.refract_roughness.set(m["refraction_roughness"])
+        mat.refract_color.set(tuple(m["refraction_color"]))
+        u.children_shapes.append(s)
+    return SDFEditor([u])
+
+
 def c3_no_aabb() -> SDFEditor:
     """c3 with every Transform.aabb off (profiling aid: no per-lane culling)."""
     ed = c3_graph32()

@@ -291,3 +291,16 @@ def test_jit_tier_up_follows_value_edits(gpu):
     assert pt.get_option("jit_tier_active") == 1.0
     check()
     pt.close()
+
+
+def test_deprecated_map_scene(gpu):
+    """The reference's saved map (assets/maps/test.json fixture) through the
+    default kernel, against the oracle."""
+    import os
+
+    from compute_path_tracer_amd.scenes import deprecated_map
+
+    ed = deprecated_map(os.path.join(os.path.dirname(__file__), "golden", "maps_test.json"))
+    gpu_img, ref = _render_pair(ed, 64, 40, 3, 6, kernel="binned_tier")
+    rms, exact = _report(gpu_img, ref)
+    assert exact == 1.0, rms

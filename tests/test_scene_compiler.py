@@ -168,3 +168,29 @@ def test_default_editor_scene():
     assert len(prog.data) == 36 and prog.data[0] == np.float32(6969.69)
     assert prog.n_ops == 3 and prog.n_aabb == 1 and prog.n_check == 1
     assert prog.data[8] == np.float32(1.3)  # aabb_exaggeration default
+
+
+GOLDEN_MAP = os.path.join(os.path.dirname(__file__), "golden", "maps_test.json")
+
+
+def test_deprecated_map_loads_and_pins_c3_room():
+    """assets/maps/test.json (the deprecated node-editor save, committed as a
+    data fixture) loads into the current editor; c3's room copies its values."""
+    from compute_path_tracer_amd.scenes import deprecated_map
+
+    ed = deprecated_map(GOLDEN_MAP)
+    (u,) = ed.header_unions
+    assert [s.name for s in u.children_shapes] == ["floor", "roof", "light", "4", "5", "6", "7", "8"]
+    assert [s.current_shape.kind for s in u.children_shapes].count("Octahedron") == 2
+    prog = ed.compile(CompData())
+    assert prog.n_aabb == 8 and prog.n_check == 8
+    room = {s.name: s for s in scenes.c3_graph32().header_unions[0].children_shapes}
+    for s in u.children_shapes:
+        if s.name not in room:
+            continue
+        r = room[s.name]
+        for get in (lambda x: x.transform.position.vals(), lambda x: x.transform.rotation.vals(),
+                    lambda x: [p.val for p in x.current_shape.params], lambda x: x.material.color.vals(),
+                    lambda x: x.material.light_col.vals(), lambda x: [x.material.brightness.val],
+                    lambda x: [x.material.specular_chance.val], lambda x: x.material.specular_color.vals()):
+            assert get(s) == get(r), s.name
