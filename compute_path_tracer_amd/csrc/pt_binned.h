@@ -288,6 +288,9 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
 // its next ray to rout at its binned position.
 template <class Map, bool ST>
 __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
+    // the staged window, once its loads have landed: [part][lane], so a
+    // refill reads a ray with 4 ds_read_b128 instead of 16 cross-lane moves
+    __shared__ uint4 W[5][64];
     const PtLaunch &L = P.L;
     const int lane = int(threadIdx.x);
     Stats<ST> st;
@@ -329,10 +332,12 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0, s2 = s0;
     uint4 s3 = make_uint4(0u, 0u, 0u, 0u);
     uint2 sh = make_uint2(0u, 0u);
+    bool in_lds = false;  // the staged window has been copied to W
     auto stage = [&]() {
         wbase = nb;
         wcnt = nc;
         wtake = 0u;
+        in_lds = false;
         if (uint32_t(lane) < wcnt) {
             const uint4 *v = reinterpret_cast<const uint4 *>(P.rin + nslot);
             const uint4 a = v[0], b = v[1], c = v[2];
@@ -369,19 +374,37 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             const int r = lane_rank(freem);
             const int src = int(wtake) + r;
             const bool got = state == ST_FREE && uint32_t(r) < take;
-            // cross-lane moves of the staged ray (every lane takes part)
-            const float a0 = __shfl(s0.x, src, 64), a1 = __shfl(s0.y, src, 64), a2 = __shfl(s0.z, src, 64),
-                        a3 = __shfl(s0.w, src, 64);
-            const float b0 = __shfl(s1.x, src, 64), b1 = __shfl(s1.y, src, 64), b2 = __shfl(s1.z, src, 64),
-                        b3 = __shfl(s1.w, src, 64);
-            const float c0 = __shfl(s2.x, src, 64), c1 = __shfl(s2.y, src, 64), c2 = __shfl(s2.z, src, 64),
-                        c3 = __shfl(s2.w, src, 64);
-            const uint32_t d0 = uint32_t(__shfl(int(s3.x), src, 64)), d1 = uint32_t(__shfl(int(s3.y), src, 64)),
-                           d2 = uint32_t(__shfl(int(s3.z), src, 64)), d3 = uint32_t(__shfl(int(s3.w), src, 64));
-            uint32_t e0 = 0u, e1 = 0u;
-            if (P.wide) {
-                e0 = uint32_t(__shfl(int(sh.x), src, 64));
-                e1 = uint32_t(__shfl(int(sh.y), src, 64));
+            if (!in_lds) {  // first refill from this window: park it in LDS (waits for its loads)
+                W[0][lane] = make_uint4(__float_as_uint(s0.x), __float_as_uint(s0.y), __float_as_uint(s0.z),
+                                        __float_as_uint(s0.w));
+                W[1][lane] = make_uint4(__float_as_uint(s1.x), __float_as_uint(s1.y), __float_as_uint(s1.z),
+                                        __float_as_uint(s1.w));
+                W[2][lane] = make_uint4(__float_as_uint(s2.x), __float_as_uint(s2.y), __float_as_uint(s2.z),
+                                        __float_as_uint(s2.w));
+                W[3][lane] = s3;
+                if (P.wide) W[4][lane] = make_uint4(sh.x, sh.y, 0u, 0u);
+                in_lds = true;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f, b0 = 0.0f, b1 = 0.0f, b2 = 0.0f, b3 = 0.0f;
+            float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
+            uint32_t d0 = 0u, d1 = 0u, d2 = 0u, d3 = 0u, e0 = 0u, e1 = 0u;
+            if (got) {
+                const uint4 wa = W[0][src], wb = W[1][src], wc = W[2][src], wd = W[3][src];
+                a0 = __uint_as_float(wa.x), a1 = __uint_as_float(wa.y), a2 = __uint_as_float(wa.z);
+                a3 = __uint_as_float(wa.w);
+                b0 = __uint_as_float(wb.x), b1 = __uint_as_float(wb.y), b2 = __uint_as_float(wb.z);
+                b3 = __uint_as_float(wb.w);
+                c0 = __uint_as_float(wc.x), c1 = __uint_as_float(wc.y), c2 = __uint_as_float(wc.z);
+                c3 = __uint_as_float(wc.w);
+                d0 = wd.x, d1 = wd.y, d2 = wd.z, d3 = wd.w;
+                if (P.wide) {
+                    const uint4 we = W[4][src];
+                    e0 = we.x;
+                    e1 = we.y;
+                }
             }
             if (got) {
                 ro = pt_f3{a0, a1, a2};
