@@ -498,7 +498,7 @@ static size_t bin_samples(const pt_ctx *c) {
         const char *v = std::getenv("PT_BIN_SAMPLES");
         return v ? std::atol(v) : 0L;
     }();
-    return env >= 64 ? size_t(env) : (size_t(1) << 27);  // 21.5 GB of HBM; larger chunks shorten per-pass tails
+    return env >= 64 ? size_t(env) : (size_t(1) << 27);  // 23.6 GB of HBM; larger chunks shorten per-pass tails
 }
 
 static void free_bin(pt_ctx *c) {

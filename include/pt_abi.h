@@ -199,7 +199,7 @@ int pt_display(pt_ctx *ctx, int format, void *out, size_t bytes);
  * rays of a chunk of frames are grouped by their bounds() check set before
  * they are marched), "shade_batch" (state-machine kernels: lanes that must
  * wait before a shading pass runs, 1..64), "bin_samples" (binned kernel:
- * samples per chunk, >= 64; device memory = 160 B per sample), "jit" (1:
+ * samples per chunk, >= 64; device memory = 176 B per sample), "jit" (1:
  * per-scene hipRTC build of the state-machine kernels, compiled at
  * pt_set_data when the topology or an identity flag changed -- the analogue
  * of remake_pipeline; 0: op-list interpreter), "jit_bake" (0: node values
