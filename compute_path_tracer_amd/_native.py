@@ -35,7 +35,7 @@ STAT_NAMES = (
     "wave_maps", "wave_shapes", "wave_iters", "lane_idle", "idle_shade", "idle_free",
     # wavefront kernel, wave-clock cycles (s_memtime) per phase, summed over waves
     "cyc_refill", "cyc_bounds", "cyc_map", "cyc_shade", "cyc_total",
-    "reserved27", "reserved28", "reserved29", "reserved30", "reserved31",
+    "culled", "wave_evals", "reserved29", "reserved30", "reserved31",
 )
 
 SYMBOLS = (

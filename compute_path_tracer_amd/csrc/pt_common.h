@@ -189,6 +189,12 @@ __device__ __forceinline__ void count_shape(Stats<ST> &st, int shape, int how) {
     st.add(how == PT_COMBINE_ASSIGN ? PT_ST_COMB_ASSIGN : (how == PT_COMBINE_UNION ? PT_ST_COMB_UNION : PT_ST_COMB_SUB));
 }
 
+template <bool ST>
+__device__ __forceinline__ void count_eval(Stats<ST> &st) {
+    if constexpr (ST)
+        if (first_active_lane()) st.add(PT_ST_WAVE_EVALS);
+}
+
 // The generated map() (sdf_editor.rs:192-210) interpreted from the op list.
 // Depth 0 is the `start` accumulator, depth 1 a header union; deeper nesting
 // spills to a private stack (scratch) that flat scenes never touch.
@@ -212,6 +218,7 @@ struct InterpMap {
                     if (n.flags & PT_NF_SCALE) d = d / n.inv;  // finalise_scale: d /= 1.0 / s
                     cur = combine(n.combine, cur, Hit{d, n.mat});
                     count_shape(st, n.shape, n.combine);
+                    count_eval(st);
                 }
             } else if (n.op == PT_OP_UNION_BEGIN) {
                 if (depth == 0) {

@@ -94,6 +94,8 @@ enum {
     PT_ST_CYC_MAP,      //   map() + state update
     PT_ST_CYC_SHADE,    //   shading + fold
     PT_ST_CYC_TOTAL,    //   whole wave
+    PT_ST_CULLED,       // lane shape evaluations dropped by the distance bound (counted in the kinds above too)
+    PT_ST_WAVE_EVALS,   // wave-level shape evaluations that ran (WAVE_SHAPES minus whole-wave culls)
     PT_ST_COUNT
 };
 

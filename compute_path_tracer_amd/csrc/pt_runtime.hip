@@ -9,12 +9,14 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <future>
 #include <map>
 #include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <new>
 #include <string>
 #include <vector>
@@ -255,6 +257,62 @@ int alloc_image(pt_ctx *c, uint32_t w, uint32_t h) {
 // once with the same rounding (see pt_device.h).
 }  // namespace
 
+// Distance-bound culling data for the scene kernels (pt_jit.cpp, DESIGN.md
+// 3.12), in PtNode.pad[0]:
+//  * shape: R' = R + 2^-12 (|R| + |m|_1), where R bounds the shape from its
+//    local origin (sdf(q) >= |q| - R: sphere r, cube |b|, torus |R1| + r,
+//    octahedron s), or NaN when the node's values are outside the range the
+//    rounding argument covers (never culled);
+//  * union begin: the matching end's 1/s when the union may drop shapes that
+//    cannot beat its parent's running distance (it combines into the parent by
+//    union, has no child unions, only assign/union shapes, all with finite
+//    R'), else NaN.
+void pt_cull_bounds(std::vector<PtNode> &nodes) {
+    const float nan = std::numeric_limits<float>::quiet_NaN();
+    const double big = 1099511627776.0;  // 2^40
+    auto fin = [&](float v) { return std::isfinite(v) && std::fabs(double(v)) <= big; };
+    for (PtNode &d : nodes) {
+        d.pad[0] = nan;
+        if (d.op != PT_OP_SHAPE) continue;
+        bool ok = std::isfinite(d.inv) && d.inv >= 0x1p-20f && d.inv <= 0x1p20f && fin(d.m[0]) && fin(d.m[1]) &&
+                  fin(d.m[2]) && fin(d.cx) && fin(d.sx) && fin(d.cy) && fin(d.sy) && fin(d.cz) && fin(d.sz);
+        double R = 0.0;
+        switch (d.shape) {
+            case PT_NODE_SPHERE: ok = ok && fin(d.size[0]); R = d.size[0]; break;
+            case PT_NODE_CUBE:
+                ok = ok && fin(d.size[0]) && fin(d.size[1]) && fin(d.size[2]) && d.size[0] >= 0.0f &&
+                     d.size[1] >= 0.0f && d.size[2] >= 0.0f;
+                R = std::sqrt(double(d.size[0]) * d.size[0] + double(d.size[1]) * d.size[1] +
+                              double(d.size[2]) * d.size[2]);
+                break;
+            case PT_NODE_TORUS:
+                ok = ok && fin(d.size[0]) && fin(d.size[1]);
+                R = std::fabs(double(d.size[0])) + double(d.size[1]);
+                break;
+            case PT_NODE_OCTAHEDRON: ok = ok && fin(d.size[0]) && d.size[0] >= 0.0f; R = d.size[0]; break;
+            default: ok = false;
+        }
+        if (!ok) continue;
+        const double m1 = std::fabs(double(d.m[0])) + std::fabs(double(d.m[1])) + std::fabs(double(d.m[2]));
+        d.pad[0] = float(R + 0x1p-12 * (std::fabs(R) + m1));
+    }
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        if (nodes[i].op != PT_OP_UNION_BEGIN) continue;
+        size_t j = i + 1;
+        bool ok = true;
+        for (; j < nodes.size() && nodes[j].op != PT_OP_UNION_END; ++j) {
+            const PtNode &c = nodes[j];
+            if (c.op != PT_OP_SHAPE || !(c.combine == PT_COMBINE_ASSIGN || c.combine == PT_COMBINE_UNION) ||
+                !std::isfinite(c.pad[0]))
+                ok = false;  // a child union, a subtraction, or a shape without a bound
+        }
+        if (j == nodes.size()) continue;
+        const PtNode &e = nodes[j];
+        ok = ok && e.combine == PT_COMBINE_UNION && std::isfinite(e.inv) && e.inv > 0.0f;
+        if (ok) nodes[i].pad[0] = e.inv;
+    }
+}
+
 int pt_derive(const std::vector<pt_op> &ops, const std::vector<pt_aabb> &aabbs, const float *data, uint32_t n,
               std::vector<PtNode> &nodes, std::vector<PtAabb> &boxes, std::vector<PtMat> &mats, std::string &err) {
     auto bad = [&](const char *msg) {
@@ -325,6 +383,7 @@ int pt_derive(const std::vector<pt_op> &ops, const std::vector<pt_aabb> &aabbs, 
             mats.push_back(m);
         }
     }
+    pt_cull_bounds(nodes);
     boxes.resize(aabbs.size());
     for (size_t i = 0; i < aabbs.size(); ++i) {
         const pt_aabb &a = aabbs[i];

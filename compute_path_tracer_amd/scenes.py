@@ -226,6 +226,43 @@ def wide_graph(seed: int = 7, unions: int = 12, per_union: int = 8) -> SDFEditor
     return ed
 
 
+def cull_stress(seed: int = 11) -> SDFEditor:
+    """c3's room plus clustered unions of every shape kind under scaled and
+    rotated union/shape transforms: the distance-bound culling of the scene
+    kernels drops shapes near its threshold.  Three unions
+    carry values that switch the rule off (a negative cube size, a 1e-7 shape
+    scale) or keep it on with a negative sphere radius."""
+    rng = np.random.default_rng(seed)
+    ed = c3_graph32()
+    kinds = (Shapes.SPHERE, Shapes.CUBE, Shapes.TORUS, Shapes.OCTAHEDRON)
+    for ui in range(6):
+        u = _union(f"cluster-{ui}", pos=(rng.uniform(-1.2, 1.2), rng.uniform(-0.6, 0.9), rng.uniform(0.5, 3.0)),
+                   rot=tuple(rng.uniform(-0.8, 0.8, 3)), scale=float(rng.uniform(0.6, 1.4)))
+        for k in range(6):
+            kind = kinds[(ui + k) % 4]
+            if kind == Shapes.CUBE:
+                size = tuple(rng.uniform(0.05, 0.3, 3))
+            elif kind == Shapes.TORUS:
+                size = (float(rng.uniform(0.1, 0.3)), float(rng.uniform(0.02, 0.1)))
+            else:
+                size = (float(rng.uniform(0.05, 0.3)),)
+            sc = float(rng.uniform(0.5, 1.6))
+            if ui == 3 and k == 2:
+                size = (0.2, -0.1, 0.2)  # degenerate cube: no bound, the union's rule is off
+                kind = Shapes.CUBE
+            if ui == 4 and k == 4:
+                sc = 1e-7  # 1/s beyond the bound's range: no bound, the union's rule is off
+            if ui == 5 and k == 1:
+                kind, size = Shapes.SPHERE, (-0.15,)  # negative radius: still bounded (R = r)
+            s = _shape(kind, pos=tuple(rng.uniform(-0.5, 0.5, 3)), rot=tuple(rng.uniform(-math.pi, math.pi, 3)),
+                       scale=sc, size=size, aabb=bool(rng.random() < 0.7), name=f"cluster-{ui}-{k}")
+            _mat(s, col=tuple(rng.uniform(0.2, 0.9, 3)), brightness=2.0 if rng.random() < 0.15 else 0.0,
+                 spec=float(rng.choice([0.0, 0.5])), rough=0.3)
+            u.children_shapes.append(s)
+        ed.header_unions.append(u)
+    return ed
+
+
 _DEPRECATED_KINDS = {"Sphere": Shapes.SPHERE, "Cube": Shapes.CUBE, "OctahedronExact": Shapes.OCTAHEDRON}
 
 
@@ -282,6 +319,7 @@ SCENES = {
     "nested": nested_demo,
     "c3_noaabb": c3_no_aabb,
     "wide": wide_graph,
+    "cull": cull_stress,
 }
 
 # BASELINE.json configs -> (scene, width, height, spp, bounces)

@@ -1,0 +1,127 @@
+"""Distance-bound culling of the scene kernels, host side.
+
+The bound data (PtNode.pad[0], pt_runtime.hip pt_cull_bounds) is read back
+from the values-baked hipRTC source (exact hex literals) and recomputed here
+from the same baked node values; the generated map() must carry the parent
+rule exactly for the unions the rule allows.  No GPU: hipRTC cross-compiles.
+The exactness of the culled images is checked on the GPU by
+test_gpu_parity.py (scene "cull" and every scene with eligible unions)."""
+import ctypes
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+from compute_path_tracer_amd import _native as N, scenes
+from compute_path_tracer_amd.sdf_editor import CompData
+
+
+def _value(tok: str) -> float:
+    tok = tok.strip()
+    if tok.startswith("__builtin_nanf"):
+        return math.nan
+    if tok.startswith("(-__builtin_inff"):
+        return -math.inf
+    if tok.startswith("__builtin_inff"):
+        return math.inf
+    if tok.endswith("u"):
+        return float(int(tok[:-1]))
+    if tok.startswith("0x") or tok.startswith("-0x"):
+        return float.fromhex(tok.rstrip("f"))
+    return float(tok.rstrip("f"))
+
+
+def _baked(scene: str, tmp_path):
+    prog = scenes.SCENES[scene]().compile(CompData())
+    dump = tmp_path / f"{scene}.hip"
+    old = {k: os.environ.get(k) for k in ("PT_JIT_BAKE", "PT_JIT_DUMP")}
+    os.environ["PT_JIT_BAKE"], os.environ["PT_JIT_DUMP"] = "1", str(dump)
+    try:
+        log = ctypes.create_string_buffer(1 << 16)
+        rc = N.lib().pt_jit_compile(prog.ops, prog.n_ops, prog.aabbs, prog.n_aabb,
+                                    prog.data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(prog.data), log,
+                                    len(log), None)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert rc == N.PT_OK, log.value.decode()
+    src = dump.read_text()
+    nodes = []
+    for m in re.finditer(r"constexpr PtNode B(\d+)\{(.*?)\};\n", src):
+        toks = [t for t in m.group(2).replace("{", ",").replace("}", ",").split(",") if t.strip()]
+        v = [_value(t) for t in toks]
+        nodes.append(dict(op=int(v[0]), shape=int(v[1]), combine=int(v[2]), inv=v[6], m=v[7:10], rot=v[10:16],
+                          size=v[16:19], pad=v[19]))
+        assert int(m.group(1)) == len(nodes) - 1
+    return src, nodes
+
+
+def _expected_shape_pad(n) -> float:
+    """pt_cull_bounds for one shape (R' = R + 2^-12 (|R| + |m|_1), or NaN)."""
+    big = 2.0 ** 40
+    fin = lambda v: math.isfinite(v) and abs(v) <= big  # noqa: E731
+    ok = math.isfinite(n["inv"]) and 2.0 ** -20 <= n["inv"] <= 2.0 ** 20 and all(map(fin, n["m"] + n["rot"]))
+    s = n["size"]
+    if n["shape"] == N.PT_NODE_SPHERE:
+        ok, R = ok and fin(s[0]), s[0]
+    elif n["shape"] == N.PT_NODE_CUBE:
+        ok = ok and all(fin(x) and x >= 0.0 for x in s)
+        R = math.sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2])
+    elif n["shape"] == N.PT_NODE_TORUS:
+        ok, R = ok and fin(s[0]) and fin(s[1]), abs(s[0]) + s[1]
+    elif n["shape"] == N.PT_NODE_OCTAHEDRON:
+        ok, R = ok and fin(s[0]) and s[0] >= 0.0, s[0]
+    else:
+        ok, R = False, 0.0
+    if not ok:
+        return math.nan
+    return float(np.float32(R + 2.0 ** -12 * (abs(R) + sum(abs(x) for x in n["m"]))))
+
+
+def _same(a: float, b: float) -> bool:
+    return (math.isnan(a) and math.isnan(b)) or a == b
+
+
+@pytest.mark.parametrize("scene", ["cull", "c3", "c2", "nested"])
+def test_bounds_match_restatement(scene, tmp_path):
+    src, nodes = _baked(scene, tmp_path)
+    assert nodes
+    for i, n in enumerate(nodes):
+        if n["op"] == N.PT_OP_SHAPE:
+            assert _same(n["pad"], _expected_shape_pad(n)), (i, n)
+        elif n["op"] == N.PT_OP_UNION_BEGIN:
+            j, ok = i + 1, True
+            while nodes[j]["op"] != N.PT_OP_UNION_END:
+                c = nodes[j]
+                if c["op"] != N.PT_OP_SHAPE or c["combine"] not in (N.PT_COMBINE_ASSIGN, N.PT_COMBINE_UNION) \
+                        or math.isnan(c["pad"]):
+                    ok = False
+                j += 1
+            e = nodes[j]
+            ok = ok and e["combine"] == N.PT_COMBINE_UNION and math.isfinite(e["inv"]) and e["inv"] > 0.0
+            assert _same(n["pad"], e["inv"] if ok else math.nan), (i, n)
+            # the rule is emitted exactly for the structurally eligible unions
+            static = all(nodes[k]["op"] == N.PT_OP_SHAPE and nodes[k]["combine"] != N.PT_COMBINE_SUBTRACTION
+                         for k in range(i + 1, j)) and e["combine"] == N.PT_COMBINE_UNION
+            assert (f"* B{i}.pad[0];" in src) == static, i
+        else:
+            assert math.isnan(n["pad"])
+
+
+def test_cull_scene_switches_the_rule_off_where_values_demand(tmp_path):
+    _, nodes = _baked("cull", tmp_path)
+    begins = [i for i, n in enumerate(nodes) if n["op"] == N.PT_OP_UNION_BEGIN]
+    # header unions: room, objects-a, objects-b (subtraction), objects-c, cluster-0..5
+    pads = [nodes[i]["pad"] for i in begins]
+    assert len(pads) == 10
+    assert math.isnan(pads[2])  # subtraction union
+    assert math.isnan(pads[7])  # cluster-3: a cube with a negative size
+    assert math.isnan(pads[8])  # cluster-4: a shape with 1/s beyond 2^20
+    assert all(math.isfinite(p) for k, p in enumerate(pads) if k not in (2, 7, 8))
+    neg = [n for n in nodes if n["op"] == N.PT_OP_SHAPE and n["shape"] == N.PT_NODE_SPHERE and n["size"][0] < 0]
+    assert neg and all(math.isfinite(n["pad"]) for n in neg)  # R = r < 0 still bounds a sphere

@@ -73,6 +73,7 @@ def _report(gpu, ref):
     ("nested", 64, 64, 3, 6),
     ("wide", 48, 32, 2, 6),        # 124 check[] entries: the high mask words
     ("c3_noaabb", 40, 24, 2, 8),   # no bounds() boxes: every mask empty, one bin
+    ("cull", 64, 40, 3, 6),        # distance-bound culling near its threshold, rule on/off per union
 ])
 def test_parity_path_trace(gpu, name, w, h, spp, bounces, kernel):
     gpu_img, ref = _render_pair(scenes.SCENES[name](), w, h, spp, bounces, kernel=kernel)
