@@ -91,6 +91,18 @@ def _same(a: float, b: float) -> bool:
 def test_bounds_match_restatement(scene, tmp_path):
     src, nodes = _baked(scene, tmp_path)
     assert nodes
+    # parent accumulator still MAXHIT when the union begins (no cull code then)
+    fresh_parent, fresh = {}, [True]
+    for i, n in enumerate(nodes):
+        if n["op"] == N.PT_OP_UNION_BEGIN:
+            fresh_parent[i] = fresh[-1]
+            fresh.append(True)
+        elif n["op"] == N.PT_OP_SHAPE:
+            fresh[-1] = False
+        else:
+            fresh.pop()
+            fresh[-1] = False
+    assert any(fresh_parent.values())  # the first header union
     for i, n in enumerate(nodes):
         if n["op"] == N.PT_OP_SHAPE:
             assert _same(n["pad"], _expected_shape_pad(n)), (i, n)
@@ -106,8 +118,9 @@ def test_bounds_match_restatement(scene, tmp_path):
             ok = ok and e["combine"] == N.PT_COMBINE_UNION and math.isfinite(e["inv"]) and e["inv"] > 0.0
             assert _same(n["pad"], e["inv"] if ok else math.nan), (i, n)
             # the rule is emitted exactly for the structurally eligible unions
+            # that have a running parent distance to test against
             static = all(nodes[k]["op"] == N.PT_OP_SHAPE and nodes[k]["combine"] != N.PT_COMBINE_SUBTRACTION
-                         for k in range(i + 1, j)) and e["combine"] == N.PT_COMBINE_UNION
+                         for k in range(i + 1, j)) and e["combine"] == N.PT_COMBINE_UNION and not fresh_parent[i]
             assert (f"* B{i}.pad[0];" in src) == static, i
         else:
             assert math.isnan(n["pad"])
