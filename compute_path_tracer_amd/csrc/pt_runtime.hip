@@ -75,13 +75,26 @@ struct pt_ctx {
     std::string tier_failed;  // a baked source that did not build (not retried)
     std::future<std::vector<char>> tier_job;  // code object (empty: compile failed)
     double tier_seconds = 0.0;
-    // binned pipeline buffers (pt_binned.h), for bin_cap samples per chunk
-    PtRay *d_ray[2] = {nullptr, nullptr};  // ping-pong: pass k reads d_ray[k & 1], writes the other
-    uint2 *d_mask_hi = nullptr;            // check[] bits 64..127 (scenes with > 64 entries)
-    uint32_t *d_key = nullptr, *d_idx = nullptr, *d_hist = nullptr, *d_offs = nullptr, *d_ctrl = nullptr;
+    // binned pipeline buffers (pt_binned.h).  A chunk's frames are split over
+    // up to kMaxLanes independent pipelines ("lanes"), each on its own stream,
+    // so one lane's memory-bound passes (shade, gen, scatter) run beside
+    // another's VALU-bound trace pass and fill its tail.  bin_cap samples per
+    // lane; the colour buffer holds the whole chunk.
+    struct BinLane {
+        PtRay *ray[2] = {nullptr, nullptr};  // ping-pong: pass k reads ray[k & 1], writes the other
+        uint2 *mask_hi = nullptr;            // check[] bits 64..127 (scenes with > 64 entries)
+        uint32_t *key = nullptr, *idx = nullptr, *hist = nullptr, *offs = nullptr, *ctrl = nullptr;
+        float4 *hitn = nullptr;  // trace -> shade: normal differences per position
+        hipStream_t stream = nullptr;
+    };
+    static constexpr int kMaxLanes = 4;
+    BinLane lane[kMaxLanes];
+    int n_lanes = 0;  // lanes allocated
     float4 *d_color = nullptr;
-    float4 *d_hitn = nullptr;  // trace -> shade: normal differences per position
     size_t bin_cap = 0, ctrl_words = 0;
+    hipStream_t xstream[kMaxLanes] = {};   // lanes 1.. streams (created on first use; lane 0 = stream)
+    hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {};
+    int bin_lanes = -1;                    // pt_set_option "bin_lanes"; -1 = env PT_BIN_LANES
     int cu_count = 0;
     bool fast_bounds = false;  // every box coordinate inside the reciprocal-division guard
     // HIP events around each trace-pass launch of the last dispatch (pairs)
@@ -560,60 +573,89 @@ static size_t bin_samples(const pt_ctx *c) {
     return env >= 64 ? size_t(env) : (size_t(1) << 27);  // 23.6 GB of HBM; larger chunks shorten per-pass tails
 }
 
+// Pipelines per chunk (1..kMaxLanes): pt_set_option "bin_lanes", else env PT_BIN_LANES.
+static int bin_lanes(const pt_ctx *c) {
+    if (c->bin_lanes >= 1 && c->bin_lanes <= pt_ctx::kMaxLanes) return c->bin_lanes;
+    static const int env = [] {
+        const char *v = std::getenv("PT_BIN_LANES");
+        const int n = v ? std::atoi(v) : 2;
+        return (n >= 1 && n <= pt_ctx::kMaxLanes) ? n : 2;
+    }();
+    return env;
+}
+
 static void free_bin(pt_ctx *c) {
-    (void)hipFree(c->d_ray[0]);
-    (void)hipFree(c->d_ray[1]);
-    (void)hipFree(c->d_mask_hi);
-    (void)hipFree(c->d_key);
-    (void)hipFree(c->d_idx);
-    (void)hipFree(c->d_hist);
-    (void)hipFree(c->d_offs);
-    (void)hipFree(c->d_ctrl);
+    for (auto &l : c->lane) {
+        (void)hipFree(l.ray[0]);
+        (void)hipFree(l.ray[1]);
+        (void)hipFree(l.mask_hi);
+        (void)hipFree(l.key);
+        (void)hipFree(l.idx);
+        (void)hipFree(l.hist);
+        (void)hipFree(l.offs);
+        (void)hipFree(l.ctrl);
+        (void)hipFree(l.hitn);
+        const hipStream_t s = l.stream;
+        l = pt_ctx::BinLane{};
+        l.stream = s;
+    }
     (void)hipFree(c->d_color);
-    (void)hipFree(c->d_hitn);
-    c->d_ray[0] = c->d_ray[1] = nullptr;
-    c->d_mask_hi = nullptr;
-    c->d_key = c->d_idx = c->d_hist = c->d_offs = c->d_ctrl = nullptr;
     c->d_color = nullptr;
-    c->d_hitn = nullptr;
+    c->n_lanes = 0;
     c->bin_cap = c->ctrl_words = 0;
 }
 
-static int ensure_bin(pt_ctx *c, size_t samples, size_t passes) {
+// Buffers for `lanes` pipelines of `samples` samples each.
+static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
     const size_t words = 4 * (passes + 1);
-    if (samples <= c->bin_cap && words <= c->ctrl_words) return PT_OK;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (samples <= c->bin_cap && words <= c->ctrl_words && lanes <= c->n_lanes) return PT_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // lane 1 joins lane 0's stream before every dispatch ends
     samples = std::max(samples, c->bin_cap);
+    lanes = std::max(lanes, c->n_lanes);
     free_bin(c);
-    if (hipMalloc(&c->d_ray[0], samples * sizeof(PtRay)) != hipSuccess ||
-        hipMalloc(&c->d_ray[1], samples * sizeof(PtRay)) != hipSuccess ||
-        hipMalloc(&c->d_mask_hi, samples * sizeof(uint2)) != hipSuccess ||
-        hipMalloc(&c->d_key, samples * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&c->d_idx, samples * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&c->d_color, samples * sizeof(float4)) != hipSuccess ||
-        hipMalloc(&c->d_hitn, samples * sizeof(float4)) != hipSuccess ||
-        hipMalloc(&c->d_hist, PT_BINS * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&c->d_offs, PT_BINS * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&c->d_ctrl, words * sizeof(uint32_t)) != hipSuccess) {
+    bool ok = hipMalloc(&c->d_color, size_t(lanes) * samples * sizeof(float4)) == hipSuccess;
+    for (int i = 0; ok && i < lanes; ++i) {
+        pt_ctx::BinLane &l = c->lane[i];
+        ok = hipMalloc(&l.ray[0], samples * sizeof(PtRay)) == hipSuccess &&
+             hipMalloc(&l.ray[1], samples * sizeof(PtRay)) == hipSuccess &&
+             hipMalloc(&l.mask_hi, samples * sizeof(uint2)) == hipSuccess &&
+             hipMalloc(&l.key, samples * sizeof(uint32_t)) == hipSuccess &&
+             hipMalloc(&l.idx, samples * sizeof(uint32_t)) == hipSuccess &&
+             hipMalloc(&l.hitn, samples * sizeof(float4)) == hipSuccess &&
+             hipMalloc(&l.hist, PT_BINS * sizeof(uint32_t)) == hipSuccess &&
+             hipMalloc(&l.offs, PT_BINS * sizeof(uint32_t)) == hipSuccess &&
+             hipMalloc(&l.ctrl, words * sizeof(uint32_t)) == hipSuccess;
+    }
+    if (!ok) {
         free_bin(c);
         (void)hipGetLastError();
         return fail(c, PT_ERR_HIP, "out of device memory for the binned pipeline");
     }
-    HIPCHK(c, hipMemsetAsync(c->d_hist, 0, PT_BINS * sizeof(uint32_t), c->stream));
+    if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+    c->lane[0].stream = c->stream;
+    for (int i = 1; i < lanes; ++i) {
+        if (!c->xstream[i]) HIPCHK(c, hipStreamCreateWithFlags(&c->xstream[i], hipStreamNonBlocking));
+        if (!c->join_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming));
+        c->lane[i].stream = c->xstream[i];
+    }
+    for (int i = 0; i < lanes; ++i)
+        HIPCHK(c, hipMemsetAsync(c->lane[i].hist, 0, PT_BINS * sizeof(uint32_t), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->n_lanes = lanes;
     c->bin_cap = samples;
     c->ctrl_words = words;
     if (!c->cu_count) HIPCHK(c, hipDeviceGetAttribute(&c->cu_count, hipDeviceAttributeMultiprocessorCount, c->device));
     return PT_OK;
 }
 
-static hipError_t record_trace_event(pt_ctx *c) {
+static hipError_t record_trace_event(pt_ctx *c, hipStream_t stream) {
     if (c->tev_used == c->tev.size()) {
         hipEvent_t e;
         const hipError_t err = hipEventCreate(&e);
         if (err != hipSuccess) return err;
         c->tev.push_back(e);
     }
-    return hipEventRecord(c->tev[c->tev_used++], c->stream);
+    return hipEventRecord(c->tev[c->tev_used++], stream);
 }
 
 // One dispatch chunk through the pass pipeline: frames are processed in
@@ -629,7 +671,9 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     }
     const uint32_t F = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, bin_samples(c) / n_pix)));
     const int passes = L.bounces + 1;
-    int rc = ensure_bin(c, size_t(n_pix) * F, size_t(passes));
+    const int lanes = int(std::min<uint32_t>(uint32_t(bin_lanes(c)), F));
+    const uint32_t FL = (F + uint32_t(lanes) - 1) / uint32_t(lanes);  // frames per lane
+    int rc = ensure_bin(c, size_t(n_pix) * FL, size_t(passes), lanes);
     if (rc != PT_OK) return rc;
     const unsigned cu = unsigned(std::max(1, c->cu_count));
     auto item_grid = [&](size_t n) {
@@ -645,86 +689,124 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     int per_cu = 0;
     if (jit) HIPCHK(c, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jf, 64, 0));
     else per_cu = pt_bin_trace_blocks_per_cu(stats);
+    static const int trace_cu_env = [] {  // A/B knob: trace blocks (waves) per CU, below the occupancy limit
+        const char *v = std::getenv("PT_TRACE_BLOCKS");
+        return v ? std::atoi(v) : 0;
+    }();
+    if (trace_cu_env > 0 && trace_cu_env < per_cu) per_cu = trace_cu_env;
     const unsigned trace_grid = cu * unsigned(std::max(1, per_cu));
+    static const int run_max = [] {  // A/B knob
+        const char *v = std::getenv("PT_BIN_RUN");
+        const int r = v ? std::atoi(v) : 256;
+        return r >= 64 ? (r / 64) * 64 : 256;
+    }();
+    static const int refill_min = [] {  // A/B knob
+        const char *v = std::getenv("PT_REFILL_MIN");
+        const int r = v ? std::atoi(v) : 4;
+        return r >= 1 && r <= 64 ? r : 4;
+    }();
+    static const unsigned shade_cu = [] {  // A/B knob: shade blocks per CU
+        const char *v = std::getenv("PT_SHADE_BLOCKS");
+        return v ? unsigned(std::atoi(v)) : 8u;
+    }();
+    const unsigned shade_grid =
+        unsigned(std::max<size_t>(1, std::min<size_t>((c->bin_cap + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK, size_t(shade_cu) * cu)));
 
     for (uint32_t done = 0; done < spp; done += F) {
         const uint32_t fr = std::min(F, spp - done);
-        const size_t n0 = size_t(n_pix) * fr;
-        PtPass P;
-        std::memset(&P, 0, sizeof P);
-        P.L = L;
-        P.L.frame0 = int32_t(uint32_t(frame0) + done);
-        P.L.last_clear0 = int32_t(uint32_t(lc0) + done);
-        P.L.spp = int32_t(fr);
-        P.rin = c->d_ray[0];
-        P.rout = c->d_ray[1];
-        P.mask_hi = c->d_mask_hi;
-        P.key = c->d_key;
-        P.idx = c->d_idx;
-        P.hist = c->d_hist;
-        P.offs = c->d_offs;
-        P.color = c->d_color;
-        P.hitn = c->d_hitn;
-        P.ctrl = c->d_ctrl;
-        P.n_src = nullptr;
-        P.n_src_const = uint32_t(n0);
-        P.n_pix = int32_t(n_pix);
-        P.frames = int32_t(fr);
-        P.wide = c->n_check > 64 ? 1 : 0;
-        static const int run_max = [] {  // A/B knob
-            const char *v = std::getenv("PT_BIN_RUN");
-            const int r = v ? std::atoi(v) : 256;
-            return r >= 64 ? (r / 64) * 64 : 256;
-        }();
-        P.run_max = run_max;
-        static const int refill_min = [] {  // A/B knob
-            const char *v = std::getenv("PT_REFILL_MIN");
-            const int r = v ? std::atoi(v) : 4;
-            return r >= 1 && r <= 64 ? r : 4;
-        }();
-        P.refill_min = refill_min;
-        pt_launch_bin(PtBinStage::Gen, P, stats, item_grid(n0), c->stream);
-        HIPCHK(c, hipGetLastError());
-        // shade the hits trace pass k wrote into d_ray[(k + 1) & 1]: ended paths
+        // the chunk's frames over the lanes: lane i renders fl[i] frames from
+        // frame offset fo[i]; its colours land in the chunk's colour buffer
+        // at that frame offset, so one fold mixes all of them in frame order
+        const int nl = int(std::min<uint32_t>(uint32_t(lanes), fr));
+        uint32_t fl[pt_ctx::kMaxLanes], fo[pt_ctx::kMaxLanes];
+        for (int i = 0; i < nl; ++i) {
+            fl[i] = fr / uint32_t(nl) + (uint32_t(i) < fr % uint32_t(nl) ? 1u : 0u);
+            fo[i] = i == 0 ? 0u : fo[i - 1] + fl[i - 1];
+        }
+        PtPass P[pt_ctx::kMaxLanes];
+        for (int i = 0; i < nl; ++i) {
+            const pt_ctx::BinLane &l = c->lane[i];
+            PtPass &p = P[i];
+            std::memset(&p, 0, sizeof p);
+            p.L = L;
+            p.L.frame0 = int32_t(uint32_t(frame0) + done + fo[i]);
+            p.L.last_clear0 = int32_t(uint32_t(lc0) + done + fo[i]);
+            p.L.spp = int32_t(fl[i]);
+            p.rin = l.ray[0];
+            p.rout = l.ray[1];
+            p.mask_hi = l.mask_hi;
+            p.key = l.key;
+            p.idx = l.idx;
+            p.hist = l.hist;
+            p.offs = l.offs;
+            p.color = c->d_color + size_t(fo[i]) * n_pix;
+            p.hitn = l.hitn;
+            p.ctrl = l.ctrl;
+            p.n_src = nullptr;
+            p.n_src_const = uint32_t(size_t(n_pix) * fl[i]);
+            p.n_pix = int32_t(n_pix);
+            p.frames = int32_t(fl[i]);
+            p.wide = c->n_check > 64 ? 1 : 0;
+            p.run_max = run_max;
+            p.refill_min = refill_min;
+        }
+        if (nl > 1) {  // lanes 1.. start after everything enqueued on the context stream so far
+            HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
+            for (int i = 1; i < nl; ++i) HIPCHK(c, hipStreamWaitEvent(c->lane[i].stream, c->fork_ev, 0));
+        }
+        for (int i = 0; i < nl; ++i) {
+            pt_launch_bin(PtBinStage::Gen, P[i], stats, item_grid(size_t(P[i].n_src_const)), c->lane[i].stream);
+            HIPCHK(c, hipGetLastError());
+        }
+        // shade the hits trace pass k wrote into ray[(k + 1) & 1]: ended paths
         // store their colour, the rest get their next ray, bounds() and bin
-        auto shade = [&](int k) -> int {
-            PtPass S = P;
+        auto shade = [&](int i, int k) -> int {
+            PtPass S = P[i];
             S.bounce = k;
-            S.rin = c->d_ray[(k + 1) & 1];
-            S.n_src = c->d_ctrl + 4 * k;
-            static const unsigned shade_cu = [] {  // A/B knob: shade blocks per CU
-                const char *v = std::getenv("PT_SHADE_BLOCKS");
-                return v ? unsigned(std::atoi(v)) : 8u;
-            }();
-            const unsigned sg = unsigned(std::max<size_t>(1, std::min<size_t>((c->bin_cap + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK,
-                                                                            size_t(shade_cu) * cu)));
-            pt_launch_bin(PtBinStage::Shade, S, stats, sg, c->stream);
+            S.rin = c->lane[i].ray[(k + 1) & 1];
+            S.n_src = c->lane[i].ctrl + 4 * k;
+            pt_launch_bin(PtBinStage::Shade, S, stats, shade_grid, c->lane[i].stream);
             HIPCHK(c, hipGetLastError());
             return PT_OK;
         };
         for (int k = 0; k < passes; ++k) {
-            // pass k: bin the rays of d_ray[k & 1] (gen's, or the shaded hits of pass k-1), trace them into the other
-            if (k > 0 && (rc = shade(k - 1)) != PT_OK) return rc;
-            P.bounce = k;
-            P.rin = c->d_ray[k & 1];
-            P.rout = c->d_ray[(k + 1) & 1];
-            P.ctrl = c->d_ctrl + 4 * k;
-            P.n_src = k == 0 ? nullptr : c->d_ctrl + 4 * (k - 1);
-            pt_launch_bin(PtBinStage::Scan, P, stats, 1, c->stream);
-            pt_launch_bin(PtBinStage::Scatter, P, stats, scatter_grid(k == 0 ? n0 : c->bin_cap), c->stream);
-            HIPCHK(c, hipGetLastError());
-            if (!stats) HIPCHK(c, record_trace_event(c));
-            if (jit) {
-                void *args[] = {&P};
-                HIPCHK(c, hipModuleLaunchKernel(jf, trace_grid, 1, 1, 64, 1, 1, 0, c->stream, args, nullptr));
-            } else {
-                pt_launch_bin(PtBinStage::Trace, P, stats, trace_grid, c->stream);
+            for (int i = 0; i < nl; ++i) {
+                // pass k: bin the rays of ray[k & 1] (gen's, or the shaded hits of pass k-1), trace them into the other
+                const pt_ctx::BinLane &l = c->lane[i];
+                PtPass &p = P[i];
+                if (k > 0 && (rc = shade(i, k - 1)) != PT_OK) return rc;
+                p.bounce = k;
+                p.rin = l.ray[k & 1];
+                p.rout = l.ray[(k + 1) & 1];
+                p.ctrl = l.ctrl + 4 * k;
+                p.n_src = k == 0 ? nullptr : l.ctrl + 4 * (k - 1);
+                pt_launch_bin(PtBinStage::Scan, p, stats, 1, l.stream);
+                pt_launch_bin(PtBinStage::Scatter, p, stats, scatter_grid(k == 0 ? p.n_src_const : c->bin_cap), l.stream);
                 HIPCHK(c, hipGetLastError());
+                if (!stats) HIPCHK(c, record_trace_event(c, l.stream));
+                if (jit) {
+                    void *args[] = {&p};
+                    HIPCHK(c, hipModuleLaunchKernel(jf, trace_grid, 1, 1, 64, 1, 1, 0, l.stream, args, nullptr));
+                } else {
+                    pt_launch_bin(PtBinStage::Trace, p, stats, trace_grid, l.stream);
+                    HIPCHK(c, hipGetLastError());
+                }
+                if (!stats) HIPCHK(c, record_trace_event(c, l.stream));
             }
-            if (!stats) HIPCHK(c, record_trace_event(c));
         }
-        if ((rc = shade(passes - 1)) != PT_OK) return rc;  // the last bounce's hits end their paths
-        pt_launch_bin(PtBinStage::Fold, P, stats, unsigned((n_pix + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK), c->stream);
+        for (int i = 0; i < nl; ++i)  // the last bounce's hits end their paths
+            if ((rc = shade(i, passes - 1)) != PT_OK) return rc;
+        for (int i = 1; i < nl; ++i) {  // the fold (and everything after) waits for every lane
+            HIPCHK(c, hipEventRecord(c->join_ev[i], c->lane[i].stream));
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->join_ev[i], 0));
+        }
+        PtPass Fp = P[0];
+        Fp.L.frame0 = int32_t(uint32_t(frame0) + done);
+        Fp.L.last_clear0 = int32_t(uint32_t(lc0) + done);
+        Fp.L.spp = int32_t(fr);
+        Fp.color = c->d_color;
+        Fp.frames = int32_t(fr);
+        pt_launch_bin(PtBinStage::Fold, Fp, stats, unsigned((n_pix + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK), c->stream);
         HIPCHK(c, hipGetLastError());
     }
     return PT_OK;
@@ -994,6 +1076,11 @@ int pt_set_option(pt_ctx *c, const char *key, int value) {
         c->bin_samples = value;
         return PT_OK;
     }
+    if (!std::strcmp(key, "bin_lanes")) {
+        if (value < 1 || value > pt_ctx::kMaxLanes) return fail(c, PT_ERR_INVALID, "bin_lanes must be in [1, 4]");
+        c->bin_lanes = value;
+        return PT_OK;
+    }
     if (!std::strcmp(key, "shade_batch")) {
         if (value < 1 || value > 64) return fail(c, PT_ERR_INVALID, "shade_batch must be in [1, 64]");
         c->shade_batch = value;
@@ -1027,7 +1114,8 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
         }
         *value = sum;
     }
-    else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * kBinBytesPerSample;
+    else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * double(c->n_lanes) * kBinBytesPerSample;
+    else if (!std::strcmp(key, "bin_lanes")) *value = double(bin_lanes(c));
     else return fail(c, PT_ERR_INVALID, std::string("unknown option ") + key);
     return PT_OK;
 }
@@ -1051,6 +1139,11 @@ void pt_destroy(pt_ctx *c) {
     (void)hipFree(c->d_mats);
     (void)hipFree(c->d_stats);
     free_bin(c);
+    for (int i = 1; i < pt_ctx::kMaxLanes; ++i) {
+        if (c->xstream[i]) (void)hipStreamDestroy(c->xstream[i]);
+        if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
+    }
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);

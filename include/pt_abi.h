@@ -199,7 +199,10 @@ int pt_display(pt_ctx *ctx, int format, void *out, size_t bytes);
  * rays of a chunk of frames are grouped by their bounds() check set before
  * they are marched), "shade_batch" (state-machine kernels: lanes that must
  * wait before a shading pass runs, 1..64), "bin_samples" (binned kernel:
- * samples per chunk, >= 64; device memory = 176 B per sample), "jit" (1:
+ * samples per chunk, >= 64; device memory = 176 B per sample), "bin_lanes"
+ * (binned kernel: 1..4 pipelines, each on its own stream, over which a
+ * chunk's frames are split, so one's memory-bound passes overlap another's
+ * trace pass), "jit" (1:
  * per-scene hipRTC build of the state-machine kernels, compiled at
  * pt_set_data when the topology or an identity flag changed -- the analogue
  * of remake_pipeline; 0: op-list interpreter), "jit_bake" (0: node values
@@ -213,9 +216,9 @@ int pt_set_option(pt_ctx *ctx, const char *key, int value);
  * "jit_seconds" (last hipRTC compile time), "jit_tier_active" /
  * "jit_tier_seconds" (values-baked build in use / its compile time),
  * "kernel", "shade_batch",
- * "bin_samples", "bin_bytes" (device memory held by the binned pipeline),
- * "trace_ms" / "trace_launches" (device time and count of the last dispatch's
- * binned trace passes, HIP events on the context stream), "display_ms"
+ * "bin_samples", "bin_lanes", "bin_bytes" (device memory held by the binned
+ * pipeline), "trace_ms" / "trace_launches" (device time and count of the last
+ * dispatch's binned trace passes, HIP events on each pipeline's stream), "display_ms"
  * (device time of the last pt_display's kernel). */
 int pt_get_option(pt_ctx *ctx, const char *key, double *value);
 /* Log of the last failed scene-kernel build ("" if none). */

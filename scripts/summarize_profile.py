@@ -3,7 +3,8 @@
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats),
 profiles/<tag>_pmc.json (per-launch counters of the hot kernel and derived
-metrics) and profiles/<tag>_summary.md.
+metrics, plus the derived metrics of the other pipeline kernels) and
+profiles/<tag>_summary.md.
 
 HBM bytes per launch follow MI355X_MICROARCH.md "HBM": FETCH_SIZE reads
 exactly half of a wide coalesced stream on gfx950 (16 B/lane loads, which is
@@ -29,34 +30,23 @@ def hot_name(name: str) -> bool:
     return any(name.startswith(h) and "stats" not in name and "<true>" not in name for h in HOT)
 
 
-def main(tag: str, src: str = None) -> None:
-    src = src or os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-    dst = os.path.join(ROOT, "profiles")
-    os.makedirs(dst, exist_ok=True)
-    ks = os.path.join(src, "kt", "kt_kernel_stats.csv")
-    shutil.copy(ks, os.path.join(dst, f"{tag}_kernel_stats.csv"))
-    stats = list(csv.DictReader(open(ks)))
-    bench_line = None
-    for line in open(os.path.join(src, "kt_bench.log")):
-        if line.startswith("{"):
-            bench_line = json.loads(line)
-    present = [r["Name"] for r in stats if hot_name(r["Name"])]
-    hot = min(present, key=lambda n: [i for i, h in enumerate(HOT) if n.startswith(h)][0]) if present else None
-    counters, launches = {}, {}
-    meta = {}
+def collect(src: str) -> dict:
+    """{kernel name: (per-launch counters, launch meta)} over every PMC pass."""
+    counters, launches, meta = {}, {}, {}
     for f in sorted(glob.glob(os.path.join(src, "pmc*", "pmc_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
-            if r["Kernel_Name"] != hot:
-                continue
-            k = r["Counter_Name"]
-            counters[k] = counters.get(k, 0.0) + float(r["Counter_Value"])
-            launches.setdefault(k, set()).add(r["Dispatch_Id"])
-            meta = {"kernel": r["Kernel_Name"], "vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
-                    "lds_bytes": int(r["LDS_Block_Size"]), "grid": int(r["Grid_Size"]),
-                    "workgroup": int(r["Workgroup_Size"])}
-    per_launch = {k: v / max(1, len(launches[k])) for k, v in counters.items()}
+            n, k = r["Kernel_Name"], r["Counter_Name"]
+            counters.setdefault(n, {})
+            counters[n][k] = counters[n].get(k, 0.0) + float(r["Counter_Value"])
+            launches.setdefault(n, {}).setdefault(k, set()).add(r["Dispatch_Id"])
+            meta[n] = {"kernel": n, "vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
+                       "lds_bytes": int(r["LDS_Block_Size"]), "grid": int(r["Grid_Size"]),
+                       "workgroup": int(r["Workgroup_Size"])}
+    return {n: ({k: v / max(1, len(launches[n][k])) for k, v in c.items()}, meta[n]) for n, c in counters.items()}
+
+
+def derive(c: dict) -> dict:
     d = {}
-    c = per_launch
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         d["hbm_bytes_per_launch"] = 2.0 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
     if "SQ_THREAD_CYCLES_VALU" in c and c.get("SQ_ACTIVE_INST_VALU"):
@@ -72,17 +62,48 @@ def main(tag: str, src: str = None) -> None:
         d["wave_time_active"] = c.get("SQ_ACTIVE_INST_ANY", 0.0) / tot
         d["wave_time_wait_issue"] = c.get("SQ_WAIT_INST_ANY", 0.0) / tot
         d["wave_time_waitcnt"] = c.get("SQ_WAIT_ANY", 0.0) / tot
-    ktime = None
-    for r in stats:
-        if r["Name"] == hot:
-            ktime = float(r["AverageNs"]) * 1e-9
+    return d
+
+
+def main(tag: str, src: str = None) -> None:
+    src = src or os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    ks = os.path.join(src, "kt", "kt_kernel_stats.csv")
+    shutil.copy(ks, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    stats = list(csv.DictReader(open(ks)))
+    bench_line = None
+    for line in open(os.path.join(src, "kt_bench.log")):
+        if line.startswith("{"):
+            bench_line = json.loads(line)
+    present = [r["Name"] for r in stats if hot_name(r["Name"])]
+    hot = min(present, key=lambda n: [i for i, h in enumerate(HOT) if n.startswith(h)][0]) if present else None
+    per_kernel = collect(src)
+    per_launch, meta = per_kernel.get(hot, ({}, {}))
+    d = derive(per_launch)
+
+    def avg_s(name):
+        t = [float(r["AverageNs"]) * 1e-9 for r in stats if r["Name"] == name]
+        return t[0] if t else None
+
+    ktime = avg_s(hot)
     if ktime and "hbm_bytes_per_launch" in d:
         d["hbm_gbs_measured"] = d["hbm_bytes_per_launch"] / ktime / 1e9
+    others = {}
+    for n, (c, _) in sorted(per_kernel.items()):
+        if n == hot or "<true>" in n or "stats" in n:
+            continue
+        od = derive(c)
+        kt = avg_s(n)
+        if kt and "hbm_bytes_per_launch" in od:
+            od["hbm_gbs_measured"] = od["hbm_bytes_per_launch"] / kt / 1e9
+        others[n] = od
     out = {"tag": tag, "kernel": meta, "per_launch_counters": per_launch, "derived": d,
            "kernel_avg_s_kernel_trace": ktime,
            "bench_config": bench_line["config"] if bench_line else None,
            "bench_value": bench_line["value"] if bench_line else None,
-           "bench_kernel_ms_hip_events": bench_line["roofline"]["kernel_ms_per_launch"] if bench_line else None}
+           "bench_kernel_ms_hip_events": bench_line["roofline"]["kernel_ms_per_launch"] if bench_line else None,
+           "other_kernels": others}
     with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     lines = [f"# rocprofv3 summary `{tag}`", "",
@@ -99,6 +120,10 @@ def main(tag: str, src: str = None) -> None:
     lines += ["", "## Derived", ""]
     for k, v in d.items():
         lines.append(f"- {k}: {v:.6g}")
+    if others:
+        lines += ["", "## Other pipeline kernels (derived, per launch)", ""]
+        for n, od in others.items():
+            lines.append(f"- `{n}`: " + ", ".join(f"{k} {v:.4g}" for k, v in od.items()))
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print(json.dumps(out["derived"], indent=1))

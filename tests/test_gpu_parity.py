@@ -35,7 +35,7 @@ def _tier_up(pt, opts):
 
 
 def _render_pair(ed, w, h, spp, bounces, debug=0, frame=1, last_clear=1, fov=1.0, aspect=None, kernel="jit",
-                 shade_batch=None, bin_samples=None):
+                 shade_batch=None, bin_samples=None, bin_lanes=None):
     prog = ed.compile(CompData())
     st = N.Settings(debug=debug, bounces=bounces, scale=1.0, fov=fov, aabb=0)
     opts = dict(KERNELS[kernel])
@@ -43,6 +43,8 @@ def _render_pair(ed, w, h, spp, bounces, debug=0, frame=1, last_clear=1, fov=1.0
         opts["shade_batch"] = shade_batch
     if bin_samples:
         opts["bin_samples"] = bin_samples
+    if bin_lanes:
+        opts["bin_lanes"] = bin_lanes
     pt = PathTracer(w, h, prog, settings=st, options=opts)
     if opts["jit"]:
         assert pt.get_option("jit_active") == 1.0, pt.jit_log()
@@ -116,6 +118,17 @@ def test_binned_sub_chunks(gpu, bin_samples):
     its sample budget (one frame when the budget is below the pixel count);
     the fold continues last_clear across them."""
     gpu_img, ref = _render_pair(scenes.c3_graph32(), 40, 24, 11, 8, kernel="binned_jit", bin_samples=bin_samples)
+    rms, exact = _report(gpu_img, ref)
+    assert exact == 1.0, rms
+
+
+@pytest.mark.parametrize("bin_lanes", [1, 2, 3, 4])
+@pytest.mark.parametrize("spp,bin_samples", [(1, None), (2, None), (11, None), (11, 3000), (7, 64)])
+def test_binned_lanes(gpu, bin_lanes, spp, bin_samples):
+    """A chunk's frames split over one to four pipelines on separate streams
+    (ragged splits, one-frame chunks, several chunks) fold to the same image."""
+    gpu_img, ref = _render_pair(scenes.c3_graph32(), 40, 24, spp, 8, kernel="binned_tier", bin_samples=bin_samples,
+                                bin_lanes=bin_lanes)
     rms, exact = _report(gpu_img, ref)
     assert exact == 1.0, rms
 
