@@ -13,12 +13,15 @@
 //   trace   persistent waves take runs of the binned slots; the slots of the
 //           next 64-ray window are prefetched one window ahead, the rays
 //           (64 B records, mask included) gathered into staging registers
-//           and handed to free lanes, which march, calc_normal and shade
-//           them; ended paths store their colour, the others write their next
-//           ray to the other ray buffer at their binned position
-//   bounds  bounds() mask + bin of every written ray (next pass), with the
-//           live rays compacted per wave
+//           and handed to free lanes, which march and calc_normal them; a
+//           miss stores the path's colour, a hit writes a hit record to the
+//           other ray buffer at its binned position
+//   shade   shading + Russian roulette of every hit record, then bounds()
+//           mask + bin of each continuing ray (next pass)
 //   fold    each pixel mixes its frames' colours in frame order
+//
+// The host splits a chunk's frames over two such pipelines on two streams
+// (pt_runtime.hip launch_binned), so their passes overlap.
 //
 // Paths are independent and the fold runs in frame order, so the schedule
 // changes nothing in the image: it is bit-identical to the other kernels.
@@ -166,24 +169,17 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
 // goes on gets its next segment's bounds() mask and bin.  Shading is taken
 // out of the trace pass, where it ran on a fraction of the lanes of a wave;
 // here, one thread per hit, it fills the VALU time this memory-latency-bound
-// pass had idle.  Each wave compacts its hit positions through an LDS queue.
+// pass had idle.
 template <bool ST>
 __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
-    __shared__ uint32_t queue[PT_BIN_BLOCK / 64][128];
     hist_zero(lh);
     Stats<ST> st;
     st.init();
     const PtLaunch &L = P.L;
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
-    const int lane = int(threadIdx.x & 63u), wv = int(threadIdx.x >> 6);
-    uint32_t *q = queue[wv];
-    uint32_t qn = 0u;  // wave-uniform queue length
-    auto work = [&](uint32_t i) {
-        const float4 *v = reinterpret_cast<const float4 *>(P.rin + i);
-        const float4 a = v[0], b = v[1], c = v[2];
-        const uint4 d = reinterpret_cast<const uint4 *>(P.rin + i)[3];
-        const float4 nd = P.hitn[i];
+    auto shade_one = [&](uint32_t i, const float4 &a, const float4 &b, const float4 &c, const uint4 &d,
+                         const float4 &nd) {
         pt_f3 ro{a.x, a.y, a.z}, rd{a.w, b.x, b.y}, thr{b.z, b.w, c.x}, ret{c.y, c.z, c.w};
         uint32_t rng = d.x;
         int seg = P.bounce;
@@ -201,22 +197,17 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         P.key[i] = k;
         atomicAdd(&lh[k], 1u);
     };
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t base = (blockIdx.x * (blockDim.x >> 6) + uint32_t(wv)) * 64u; base < n; base += waves * 64u) {
-        const uint32_t i = base + uint32_t(lane);
-        const bool live = i < n && P.key[i] == PT_BIN_HIT;
-        const uint64_t lm = __ballot(live);
-        if (live) q[qn + uint32_t(lane_rank(lm))] = i;
-        qn += uint32_t(__popcll(lm));
-        __builtin_amdgcn_wave_barrier();
-        if (qn >= 64u) {
-            qn -= 64u;
-            work(q[qn + uint32_t(lane)]);
-            __builtin_amdgcn_wave_barrier();
-        }
+    // Nearly every position holds a hit (misses end in the trace pass), so
+    // each thread takes one position and loads its record together with the
+    // marker: one memory round trip instead of two.
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 *v = reinterpret_cast<const float4 *>(P.rin + i);
+        const uint32_t key = P.key[i];
+        const float4 a = v[0], b = v[1], c = v[2];
+        const uint4 d = reinterpret_cast<const uint4 *>(P.rin + i)[3];
+        const float4 nd = P.hitn[i];
+        if (key == PT_BIN_HIT) shade_one(i, a, b, c, d, nd);
     }
-    __builtin_amdgcn_wave_barrier();
-    if (uint32_t(lane) < qn) work(q[lane]);
     hist_flush(lh, P.hist);
     flush_stats<ST>(L, st);
 }
