@@ -5,4 +5,10 @@ import sys
 
 line = [l for l in open(sys.argv[1]).read().splitlines() if l.startswith("{")][-1]
 d = json.loads(line)
-print(d["value"], d["roofline"]["kernel_ms_per_launch"], json.dumps(d.get("schedule", {})))
+w = d.get("work", {})
+cull = {}
+if w.get("xform_shape"):
+    cull = {"lane_culled": round(w["culled"] / w["xform_shape"], 4),
+            "wave_evals_per_shape": round(w["wave_evals"] / max(1, w["wave_shapes"]), 4),
+            "wave_evals_per_map": round(w["wave_evals"] / max(1, w["wave_maps"]), 3)}
+print(d["value"], d["roofline"]["kernel_ms_per_launch"], json.dumps(d.get("schedule", {})), json.dumps(cull))
