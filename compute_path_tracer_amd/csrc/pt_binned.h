@@ -170,7 +170,14 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
 // out of the trace pass, where it ran on a fraction of the lanes of a wave;
 // here, one thread per hit, it fills the VALU time this memory-latency-bound
 // pass had idle.
-template <bool ST>
+//
+// TAPS = false (PtPass taps_in_shade, scene kernels only): the trace pass
+// stopped at the hit, and this pass evaluates calc_normal's six taps itself
+// (test_compute.glsl:57-66) with Map = JitMapB: all lanes of a wave tap
+// together, and the per-hit map() bound (pt_path.h tap_bound, from the hit
+// record) lets each tap drop every shape that provably lies farther away
+// (DESIGN.md 3.13).
+template <class Map, bool ST, bool TAPS>
 __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
     hist_zero(lh);
@@ -183,7 +190,32 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         pt_f3 ro{a.x, a.y, a.z}, rd{a.w, b.x, b.y}, thr{b.z, b.w, c.x}, ret{c.y, c.z, c.w};
         uint32_t rng = d.x;
         int seg = P.bounce;
-        const bool done = shade_lane<ST>(L.mats, L.bounces, int(d.z), nd.x, nd.y, nd.z, 0, rng, ro, rd, thr, ret, seg, st);
+        float dv0 = nd.x, dv1 = nd.y, dv2 = nd.z;
+        int mat = int(d.z);
+        if constexpr (!TAPS) {
+            // hit record: d.z/d.w = check[] bits 0..63, nd = {tap bound, material, check[] bits 64..127}
+            const Check ck{uint64_t(d.z) | (uint64_t(d.w) << 32),
+                           uint64_t(__float_as_uint(nd.z)) | (uint64_t(__float_as_uint(nd.w)) << 32)};
+            const float bnd = nd.x;
+            mat = int(__float_as_uint(nd.y));
+            float dp = 0.0f;
+#pragma unroll 1
+            for (int k = 0; k < 6; ++k) {
+                float qx, qy, qz;
+                map_point(ST_NORMAL, k, ro, rd, 0.0f, qx, qy, qz);
+                const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, bnd, st);
+                if ((k & 1) == 0) {
+                    dp = h.d;  // d(p + e)
+                } else {
+                    const float dd = dp - h.d;
+                    if (k == 1) dv0 = dd;
+                    else if (k == 3) dv1 = dd;
+                    else dv2 = dd;
+                }
+            }
+            st.add(PT_ST_NORMAL_MAPS, 6);
+        }
+        const bool done = shade_lane<ST>(L.mats, L.bounces, mat, dv0, dv1, dv2, 0, rng, ro, rd, thr, ret, seg, st);
         if (done) {
             const pt_f3 col = final_color(L.debug, seg, L.bounces, ret);
             P.color[d.y] = make_float4(col.x, col.y, col.z, 0.0f);
@@ -277,7 +309,10 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
 // moves.  Lanes run the MARCH -> NORMAL -> SHADE state machine of pt_path.h;
 // a shaded path either ends (colour stored, end marker written) or writes
 // its next ray to rout at its binned position.
-template <class Map, bool ST>
+//
+// TAPS = false: a lane stops at the hit (calc_point) and writes the hit
+// record for the shade pass, which evaluates the normal taps (bin_shade_body).
+template <class Map, bool ST, bool TAPS = true>
 __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     // the staged window, once its loads have landed: [part][lane], so a
     // refill reads a ray with 4 ds_read_b128 instead of 16 cross-lane moves
@@ -429,8 +464,14 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             if (mapping) {
                 float qx, qy, qz;
                 map_point(state, step, ro, rd, t, qx, qy, qz);
-                const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, st);
+                const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, __builtin_inff(), st);
                 after_map<ST>(h, state, step, t, ro, rd, mat, dv0, dv1, dv2, st);
+                if constexpr (!TAPS) {
+                    if (state == ST_NORMAL) {  // hit: the shade pass takes the taps
+                        dv0 = tap_bound(h.d, qx, qy, qz, t, L.bound_k);
+                        state = ST_SHADE;
+                    }
+                }
             }
         }
         tm = st.lap(PT_ST_CYC_MAP, tm);
@@ -443,8 +484,14 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
                 P.key[pos] = PT_BIN_NONE;
             } else {
-                store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, uint32_t(mat), 0u);
-                P.hitn[pos] = make_float4(dv0, dv1, dv2, 0.0f);
+                if constexpr (TAPS) {
+                    store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, uint32_t(mat), 0u);
+                    P.hitn[pos] = make_float4(dv0, dv1, dv2, 0.0f);
+                } else {  // hit point + check[] + tap bound + material (bin_shade_body)
+                    store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, uint32_t(ck.lo), uint32_t(ck.lo >> 32));
+                    P.hitn[pos] = make_float4(dv0, __uint_as_float(uint32_t(mat)), __uint_as_float(uint32_t(ck.hi)),
+                                              __uint_as_float(uint32_t(ck.hi >> 32)));
+                }
                 P.key[pos] = PT_BIN_HIT;
             }
             state = ST_FREE;

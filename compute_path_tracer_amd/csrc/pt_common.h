@@ -115,6 +115,17 @@ __device__ __forceinline__ void xform(const PtNode &n, float &x, float &y, float
     if (f & PT_NF_RZ) xform_f<PT_NF_RZ>(n, x, y, z);
 }
 
+// sdCube (shapes.glsl:5-9) from q = abs(p) - b and qm = max(q): the
+// bound-culled scene map computes q first for its test.
+__device__ __forceinline__ float cube_from_q(float qx, float qy, float qz, float qm) {
+    const float mx = pt_gmax(qx, 0.0f), my = pt_gmax(qy, 0.0f), mz = pt_gmax(qz, 0.0f);
+    return pt_sqrt(mx * mx + my * my + mz * mz) + pt_gmin(qm, 0.0f);
+}
+
+// cull target: the smaller of the parent's running distance a and the
+// point's map() bound b; a NaN bound leaves a
+__device__ __forceinline__ float cull_target(float a, float b) { return b < a ? b : a; }
+
 // SDFs, shapes.glsl:1-25 (+ torus extension)
 template <int K>
 __device__ __forceinline__ float sdf_k(const PtNode &n, float x, float y, float z) {
@@ -122,8 +133,7 @@ __device__ __forceinline__ float sdf_k(const PtNode &n, float x, float y, float 
         return pt_sqrt(x * x + y * y + z * z) - n.size[0];
     } else if constexpr (K == PT_NODE_CUBE) {
         const float qx = fabsf(x) - n.size[0], qy = fabsf(y) - n.size[1], qz = fabsf(z) - n.size[2];
-        const float mx = pt_gmax(qx, 0.0f), my = pt_gmax(qy, 0.0f), mz = pt_gmax(qz, 0.0f);
-        return pt_sqrt(mx * mx + my * my + mz * mz) + pt_gmin(pt_gmax(qx, pt_gmax(qy, qz)), 0.0f);
+        return cube_from_q(qx, qy, qz, pt_gmax(qx, pt_gmax(qy, qz)));
     } else if constexpr (K == PT_NODE_TORUS) {
         const float qx = pt_sqrt(x * x + z * z) - n.size[0];
         return pt_sqrt(qx * qx + y * y) - n.size[1];
@@ -200,7 +210,8 @@ __device__ __forceinline__ void count_eval(Stats<ST> &st) {
 // spills to a private stack (scratch) that flat scenes never touch.
 struct InterpMap {
     template <bool ST>
-    static __device__ Hit eval(const PtLaunch &L, float qx, float qy, float qz, const Check &ck, Stats<ST> &st) {
+    static __device__ Hit eval(const PtLaunch &L, float qx, float qy, float qz, const Check &ck, float /*bnd*/,
+                               Stats<ST> &st) {
         Hit cur{kMaxHit, 0};
         Hit s0{kMaxHit, 0};
         float px = qx, py = qy, pz = qz;

@@ -124,6 +124,7 @@ struct PtLaunch {
     int32_t kernel;          // PT_KERNEL_* (0 = choose)
     int32_t shade_batch;     // wavefront kernel: shade when >= this many lanes wait
     int32_t fast_bounds;     // every box coordinate passes pt_div_coord_ok (reciprocal slab divisions allowed)
+    float bound_k;           // map() bound margin: the scene's transform-chain magnitude (NaN: no bound; pt_bound_k)
 };
 
 #define PT_KERNEL_AUTO 0

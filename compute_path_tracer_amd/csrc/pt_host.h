@@ -21,6 +21,9 @@ void pt_launch_display(const float *img, uint32_t w, uint32_t h, int fmt, void *
 int pt_derive(const std::vector<pt_op> &ops, const std::vector<pt_aabb> &aabbs, const float *data, uint32_t n,
               std::vector<PtNode> &nodes, std::vector<PtAabb> &boxes, std::vector<PtMat> &mats, std::string &err);
 
+// Margin constant of the map() bound; NaN: no bound.
+float pt_bound_k(const std::vector<PtNode> &nodes);
+
 // Scene-specialised kernels (hipRTC).
 struct PtJitModule {
     hipModule_t module = nullptr;
@@ -28,6 +31,10 @@ struct PtJitModule {
     hipFunction_t render_stats = nullptr;
     hipFunction_t trace = nullptr;        // binned pipeline trace pass (pt_binned.h)
     hipFunction_t trace_stats = nullptr;
+    hipFunction_t trace_m = nullptr;        // march-only trace pass (normal taps in the shade pass)
+    hipFunction_t trace_m_stats = nullptr;
+    hipFunction_t shade_t = nullptr;        // shade pass with the normal taps (JitMapB)
+    hipFunction_t shade_t_stats = nullptr;
     std::string key;  // generated source
 };
 

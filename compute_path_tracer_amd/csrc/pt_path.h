@@ -111,6 +111,20 @@ __device__ __forceinline__ void after_map(const Hit &h, int &state, int &step, f
     }
 }
 
+// Upper bound on map() at every calc_normal tap of a hit:
+// the march's last map() value was d at point q (t: the ray parameter after
+// t += d), the hit point is |d| further along the ray and each tap e = 1e-4
+// from it.  map() is 1-Lipschitz (a min/max/assign composition of exact SDFs
+// under rotations, scales and translations) up to the rotation constants'
+// rounding (x(1 + 2^-16)); mg covers the f32 rounding of the two evaluations
+// and of the point arithmetic: a few tens of ulp of |q|_1 + |d| + t + bk,
+// bk = the scene's transform-chain magnitude (pt_bound_k; NaN: no bound).
+__device__ __forceinline__ float tap_bound(float d, float qx, float qy, float qz, float t, float bk) {
+    const float ad = fabsf(d);
+    const float mg = 0x1p-10f * (fabsf(qx) + fabsf(qy) + fabsf(qz) + ad + fabsf(t) + bk);
+    return ((d + ad) * 0x1.0001p+0f + mg) + 0x1.a38p-14f;  // + e = 1e-4 (x(1 + 2^-16), rounded up)
+}
+
 // Shading of a hit and Russian roulette (test_compute.glsl:116-159).
 // Returns true when the path ends here (miss: step < 0, roulette, or the
 // bounce limit); otherwise ro/rd/thr hold the next segment's ray and seg was

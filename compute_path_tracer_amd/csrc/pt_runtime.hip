@@ -95,8 +95,10 @@ struct pt_ctx {
     hipStream_t xstream[kMaxLanes] = {};   // lanes 1.. streams (created on first use; lane 0 = stream)
     hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {};
     int bin_lanes = -1;                    // pt_set_option "bin_lanes"; -1 = env PT_BIN_LANES
+    int shade_taps = -1;                   // pt_set_option "shade_taps"; -1 = env PT_SHADE_TAPS
     int cu_count = 0;
     bool fast_bounds = false;  // every box coordinate inside the reciprocal-division guard
+    float bound_k = 0.0f;      // pt_bound_k of the uploaded scene (NaN: no map() bound)
     // HIP events around each trace-pass launch of the last dispatch (pairs)
     std::vector<hipEvent_t> tev;
     size_t tev_used = 0;
@@ -326,6 +328,53 @@ void pt_cull_bounds(std::vector<PtNode> &nodes) {
     }
 }
 
+// Margin constant of the map() bound (pt_path.h tap_bound):
+// the largest transform-chain magnitude of any shape in world units -- the
+// |pos| of every enclosing union and of the shape, plus the shape's radius
+// bound R, each in world units.  The rounding error of a map() evaluation at
+// q is a few tens of ulp of |q|_1 + K; the kernels' margin is 2^-10 times
+// that.  NaN (no bound) when any 1/s is outside [1/2, 2] or any value is
+// beyond 2^20.
+float pt_bound_k(const std::vector<PtNode> &nodes) {
+    const float nan = std::numeric_limits<float>::quiet_NaN();
+    auto fin = [](double v) { return std::isfinite(v) && std::fabs(v) <= 1048576.0; };
+    double K = 0.0;
+    std::vector<double> scale(1, 1.0), reach(1, 0.0);  // world units per local unit; |pos| chain so far
+    for (const PtNode &d : nodes) {
+        if (d.op == PT_OP_UNION_END) {
+            if (scale.size() > 1) {
+                scale.pop_back();
+                reach.pop_back();
+            }
+            continue;
+        }
+        if (!(std::isfinite(d.inv) && d.inv >= 0.5f && d.inv <= 2.0f)) return nan;
+        for (float v : {d.m[0], d.m[1], d.m[2], d.size[0], d.size[1], d.size[2]})
+            if (!fin(v)) return nan;
+        const double sc = scale.back() / double(d.inv);  // this node's local unit in world units
+        const double r = reach.back() + (std::fabs(double(d.m[0])) + std::fabs(double(d.m[1])) +
+                                         std::fabs(double(d.m[2]))) * sc;
+        if (d.op == PT_OP_UNION_BEGIN) {
+            scale.push_back(sc);
+            reach.push_back(r);
+            continue;
+        }
+        double R;
+        switch (d.shape) {
+            case PT_NODE_SPHERE: R = std::fabs(double(d.size[0])); break;
+            case PT_NODE_CUBE:
+                R = std::sqrt(double(d.size[0]) * d.size[0] + double(d.size[1]) * d.size[1] +
+                              double(d.size[2]) * d.size[2]);
+                break;
+            case PT_NODE_TORUS: R = std::fabs(double(d.size[0])) + std::fabs(double(d.size[1])); break;
+            case PT_NODE_OCTAHEDRON: R = std::fabs(double(d.size[0])); break;
+            default: return nan;
+        }
+        K = std::max(K, r + R * sc);
+    }
+    return float(K * (1.0 + 0x1p-20));
+}
+
 int pt_derive(const std::vector<pt_op> &ops, const std::vector<pt_aabb> &aabbs, const float *data, uint32_t n,
               std::vector<PtNode> &nodes, std::vector<PtAabb> &boxes, std::vector<PtMat> &mats, std::string &err) {
     auto bad = [&](const char *msg) {
@@ -543,6 +592,7 @@ int pt_set_data(pt_ctx *c, const float *data, uint32_t n) {
     HIPCHK(c, hipMemcpyAsync(c->d_mats, mats.data(), mats.size() * sizeof(PtMat), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->have_data = true;
+    c->bound_k = pt_bound_k(nodes);
     c->fast_bounds = true;
     for (const PtAabb &b : boxes)
         for (int k = 0; k < 3; ++k)
@@ -582,6 +632,17 @@ static int bin_lanes(const pt_ctx *c) {
         return (n >= 1 && n <= pt_ctx::kMaxLanes) ? n : 2;
     }();
     return env;
+}
+
+// Normal taps in the shade pass (scene kernels only): pt_set_option
+// "shade_taps", else env PT_SHADE_TAPS.
+static bool shade_taps(const pt_ctx *c) {
+    if (c->shade_taps >= 0) return c->shade_taps != 0;
+    static const int env = [] {
+        const char *v = std::getenv("PT_SHADE_TAPS");
+        return v ? std::atoi(v) : 1;
+    }();
+    return env != 0;
 }
 
 static void free_bin(pt_ctx *c) {
@@ -685,7 +746,11 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     };
     const PtJitModule *jm = jit_active(c);
     const bool jit = jm != nullptr;
-    hipFunction_t jf = jit ? (stats ? jm->trace_stats : jm->trace) : nullptr;
+    // normal taps in the shade pass: march-only trace + tapping shade (scene kernels)
+    const bool taps_shade = jit && shade_taps(c);
+    hipFunction_t jf = jit ? (taps_shade ? (stats ? jm->trace_m_stats : jm->trace_m)
+                                         : (stats ? jm->trace_stats : jm->trace))
+                           : nullptr;
     int per_cu = 0;
     if (jit) HIPCHK(c, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jf, 64, 0));
     else per_cu = pt_bin_trace_blocks_per_cu(stats);
@@ -765,8 +830,14 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             S.bounce = k;
             S.rin = c->lane[i].ray[(k + 1) & 1];
             S.n_src = c->lane[i].ctrl + 4 * k;
-            pt_launch_bin(PtBinStage::Shade, S, stats, shade_grid, c->lane[i].stream);
-            HIPCHK(c, hipGetLastError());
+            if (taps_shade) {
+                void *args[] = {&S};
+                HIPCHK(c, hipModuleLaunchKernel(stats ? jm->shade_t_stats : jm->shade_t, shade_grid, 1, 1, PT_BIN_BLOCK,
+                                                1, 1, 0, c->lane[i].stream, args, nullptr));
+            } else {
+                pt_launch_bin(PtBinStage::Shade, S, stats, shade_grid, c->lane[i].stream);
+                HIPCHK(c, hipGetLastError());
+            }
             return PT_OK;
         };
         for (int k = 0; k < passes; ++k) {
@@ -839,6 +910,7 @@ static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, u
     L.nodes = c->d_nodes;
     L.aabbs = c->d_aabbs;
     L.fast_bounds = c->fast_bounds ? 1 : 0;
+    L.bound_k = c->bound_k;
     L.mats = c->d_mats;
     L.accum = c->accum;
     L.n_nodes = int32_t(c->ops.size());
@@ -1081,6 +1153,11 @@ int pt_set_option(pt_ctx *c, const char *key, int value) {
         c->bin_lanes = value;
         return PT_OK;
     }
+    if (!std::strcmp(key, "shade_taps")) {
+        if (value < 0 || value > 1) return fail(c, PT_ERR_INVALID, "shade_taps must be 0 or 1");
+        c->shade_taps = value;
+        return PT_OK;
+    }
     if (!std::strcmp(key, "shade_batch")) {
         if (value < 1 || value > 64) return fail(c, PT_ERR_INVALID, "shade_batch must be in [1, 64]");
         c->shade_batch = value;
@@ -1116,6 +1193,7 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     }
     else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * double(c->n_lanes) * kBinBytesPerSample;
     else if (!std::strcmp(key, "bin_lanes")) *value = double(bin_lanes(c));
+    else if (!std::strcmp(key, "shade_taps")) *value = shade_taps(c) ? 1.0 : 0.0;
     else return fail(c, PT_ERR_INVALID, std::string("unknown option ") + key);
     return PT_OK;
 }

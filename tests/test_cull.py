@@ -52,7 +52,8 @@ def _baked(scene: str, tmp_path):
     assert rc == N.PT_OK, log.value.decode()
     src = dump.read_text()
     nodes = []
-    for m in re.finditer(r"constexpr PtNode B(\d+)\{(.*?)\};\n", src):
+    # the node literals of the first map (JitMap); JitMapB repeats them
+    for m in re.finditer(r"constexpr PtNode B(\d+)\{(.*?)\};\n", src[:src.index("struct JitMapB")]):
         toks = [t for t in m.group(2).replace("{", ",").replace("}", ",").split(",") if t.strip()]
         v = [_value(t) for t in toks]
         nodes.append(dict(op=int(v[0]), shape=int(v[1]), combine=int(v[2]), inv=v[6], m=v[7:10], rot=v[10:16],
@@ -103,6 +104,23 @@ def test_bounds_match_restatement(scene, tmp_path):
             fresh.pop()
             fresh[-1] = False
     assert any(fresh_parent.values())  # the first header union
+    src, src_b = src[:src.index("struct JitMapB")], src[src.index("struct JitMapB"):]
+    # JitMapB's bound rule: top-level unions whose later
+    # top-level combines are all unions
+    top, depth = [], 0
+    for i, n in enumerate(nodes):
+        if n["op"] == N.PT_OP_UNION_BEGIN:
+            if depth == 0:
+                start = i
+            depth += 1
+        elif n["op"] == N.PT_OP_UNION_END:
+            depth -= 1
+            if depth == 0:
+                top.append((start, n["combine"]))
+    use_bnd, later = {}, True
+    for start, comb in reversed(top):
+        use_bnd[start] = later
+        later = later and comb == N.PT_COMBINE_UNION
     for i, n in enumerate(nodes):
         if n["op"] == N.PT_OP_SHAPE:
             assert _same(n["pad"], _expected_shape_pad(n)), (i, n)
@@ -122,6 +140,11 @@ def test_bounds_match_restatement(scene, tmp_path):
             static = all(nodes[k]["op"] == N.PT_OP_SHAPE and nodes[k]["combine"] != N.PT_COMBINE_SUBTRACTION
                          for k in range(i + 1, j)) and e["combine"] == N.PT_COMBINE_UNION and not fresh_parent[i]
             assert (f"* B{i}.pad[0];" in src) == static, i
+            eligible = static or (fresh_parent[i] and use_bnd.get(i, False) and all(
+                nodes[k]["op"] == N.PT_OP_SHAPE and nodes[k]["combine"] != N.PT_COMBINE_SUBTRACTION
+                for k in range(i + 1, j)) and e["combine"] == N.PT_COMBINE_UNION)
+            assert (f"* B{i}.pad[0];" in src_b) == eligible, i
+            assert (f"cull_target(h0.d, bnd) * B{i}.pad[0];" in src_b) == (eligible and use_bnd.get(i, False)), i
         else:
             assert math.isnan(n["pad"])
 

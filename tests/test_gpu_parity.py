@@ -23,8 +23,10 @@ KERNELS = {"simple": {"kernel": "simple", "jit": 0}, "wave": {"kernel": "wave", 
            "jit": {"kernel": "wave", "jit": 1, "jit_bake": 0}, "binned": {"kernel": "binned", "jit": 0},
            "binned_jit": {"kernel": "binned", "jit": 1, "jit_bake": 0},
            "binned_bake": {"kernel": "binned", "jit": 1, "jit_bake": 1},
-           "binned_tier": {"kernel": "binned", "jit": 1, "jit_bake": 2}}
-ALL = ["simple", "wave", "jit", "binned", "binned_jit", "binned_bake", "binned_tier"]
+           "binned_tier": {"kernel": "binned", "jit": 1, "jit_bake": 2},
+           # normal taps in the trace pass instead of the shade pass
+           "binned_trace_taps": {"kernel": "binned", "jit": 1, "jit_bake": 2, "shade_taps": 0}}
+ALL = ["simple", "wave", "jit", "binned", "binned_jit", "binned_bake", "binned_tier", "binned_trace_taps"]
 
 
 def _tier_up(pt, opts):
