@@ -46,27 +46,44 @@ W_CAMERA = 25
 W_ACCUM = 10
 
 
-def trace_flops(st: dict) -> float:
-    """The part of algorithmic_flops() done by the march/normal/shade kernel
-    (the binned pipeline's trace passes): everything but bounds() and the
-    camera ray / accumulation (gen, bounds and fold kernels)."""
-    return algorithmic_flops(st) - W_AABB * st["aabb_tests"] - (W_CAMERA + W_ACCUM) * st["samples"]
+def trace_flops(st: dict, taps: dict) -> float:
+    """The part of algorithmic_flops() done by the binned pipeline's trace
+    passes: the march (and calc_normal when its taps run there): everything
+    but bounds() and shading (shade pass), the camera ray (gen) and the
+    accumulation (fold), and the map() work of the shade pass's normal taps
+    (`taps`: the tap share of the stats run, PathTracer.tap_stats)."""
+    return (algorithmic_flops(st) - W_AABB * st["aabb_tests"] - W_SHADE * st["shaded"]
+            - (W_CAMERA + W_ACCUM) * st["samples"] - map_flops(taps) - W_NORMAL * (taps["normal_maps"] // 6))
 
 
-def algorithmic_flops(st: dict) -> float:
+def map_flops(st: dict) -> float:
+    """map() work: transforms, finalise, SDFs and combines."""
     xf = st["xform_union"] + st["xform_shape"]
     f = W_XFORM * xf + W_FINALISE * xf
     f += sum(w * st[k] for k, w in W_SDF.items())
     f += sum(w * st[k] for k, w in W_COMB.items())
+    return float(f)
+
+
+def algorithmic_flops(st: dict) -> float:
+    f = map_flops(st)
     f += W_MARCH * st["march_steps"] + W_NORMAL * (st["normal_maps"] // 6) + W_AABB * st["aabb_tests"]
     f += W_SHADE * st["shaded"] + (W_CAMERA + W_ACCUM) * st["samples"]
     return float(f)
 
 
-def schedule_metrics(st: dict) -> dict:
-    """SIMD efficiency of the wavefront schedule from the instrumented run."""
+def schedule_metrics(st_all: dict, taps: dict) -> dict:
+    """SIMD efficiency of the wavefront schedule from the instrumented run:
+    the trace passes (st_all minus the shade pass's normal taps), and the
+    taps' own wave-level shape evaluations."""
+    st = {k: v - taps.get(k, 0) for k, v in st_all.items()}
     maps = st["march_steps"] + st["normal_maps"]
     out = {}
+    if taps.get("normal_maps"):
+        out["shade_taps"] = {"lane_shapes_per_map": round(taps["xform_shape"] / taps["normal_maps"], 3),
+                             "lane_evals_per_map": round((taps["xform_shape"] - taps["culled"]) / taps["normal_maps"], 3),
+                             "wave_shapes_per_map": round(taps["wave_shapes"] / max(1, taps["wave_maps"]), 3),
+                             "wave_evals_per_map": round(taps["wave_evals"] / max(1, taps["wave_maps"]), 3)}
     if st.get("wave_shapes"):
         out["map_lane_util"] = round(st["xform_shape"] / (64.0 * st["wave_shapes"]), 4)
         out["wave_shapes_per_map"] = round(st["wave_shapes"] / max(1, st["wave_maps"]), 3)
@@ -193,6 +210,7 @@ def main() -> None:
 
     # algorithmic work per step from the instrumented kernel (outside timing)
     st = pt.stats(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), spp_step)
+    taps = pt.tap_stats()  # the shade pass's normal-tap share of st
 
     for _ in range(args.warmup):
         step()
@@ -252,12 +270,13 @@ def main() -> None:
     rank_pixels = st["samples"] / max(1, spp_step)
     bytes_per_launch = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per dispatch
     jit = bool(pt.get_option("jit_active"))
+    shade_taps = bool(pt.get_option("shade_taps")) and jit
     if trace_n:  # dominant kernel: the binned trace pass (flops of its passes / their device time)
-        hot = "pt_bin_trace_jit" if jit else "pt_bin_trace_kernel"
+        hot = ("pt_bin_trace_m_jit" if shade_taps else "pt_bin_trace_jit") if jit else "pt_bin_trace_kernel"
         launches = float(np.mean(trace_n))
         t_ms = float(np.mean(trace_ms))
         k_ms = t_ms / launches
-        achieved_tf = trace_flops(st) / (t_ms * 1e-3) / 1e12
+        achieved_tf = trace_flops(st, taps) / (t_ms * 1e-3) / 1e12
     else:  # the tile-resident kernels do the whole path in one launch
         hot = "pt_wave_jit" if jit else "pt_wave_kernel"
         launches, t_ms, k_ms = 1.0, d_ms, d_ms
@@ -285,7 +304,8 @@ def main() -> None:
                      "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_TFLOPS, 4), "traffic": None,
                      "traffic_source": None,
                      "algorithmic_flops_per_sample": round(flops_step / max(1, st["samples"]), 1),
-                     "kernel_flops_per_launch": round((trace_flops(st) if trace_n else flops_step) / launches),
+                     "kernel_flops_per_launch": round((trace_flops(st, taps) if trace_n else flops_step) / launches),
+                     "shade_tap_flops_per_step": round(map_flops(taps) + W_NORMAL * (taps["normal_maps"] // 6)),
                      "frac_vs_78_6": round(achieved_tf / PEAK_F32_TFLOPS_SURVEY_NONPACKED, 4),
                      "kernel_ms_per_launch": round(k_ms, 3), "kernel_launches_per_step": launches,
                      "dispatch_ms_per_step": round(d_ms, 3),
@@ -293,7 +313,7 @@ def main() -> None:
         "hbm": {"achieved": round(achieved_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "algorithmic_bytes_per_launch": bytes_per_launch},
         "work": st,
-        "schedule": schedule_metrics(st),
+        "schedule": schedule_metrics(st, taps),
         "jit": {"active": jit, "compile_s": round(pt.get_option("jit_seconds"), 3),
                 "tier_active": bool(pt.get_option("jit_tier_active")),
                 "tier_compile_s": round(pt.get_option("jit_tier_seconds"), 3)},

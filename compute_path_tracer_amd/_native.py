@@ -38,6 +38,8 @@ STAT_NAMES = (
     "culled", "wave_evals", "reserved29", "reserved30", "reserved31",
 )
 
+PT_ST_COUNT = STAT_NAMES.index("reserved29")  # device counters (pt_device.h PT_ST_COUNT)
+
 SYMBOLS = (
     "pt_compile_scene", "pt_create", "pt_resize_clear", "pt_set_program", "pt_set_data", "pt_set_tiles",
     "pt_dispatch", "pt_read_accum", "pt_accum_device_ptr", "pt_get_size", "pt_comm_get_unique_id",

@@ -183,6 +183,8 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     hist_zero(lh);
     Stats<ST> st;
     st.init();
+    Stats<ST> stt;  // the normal taps' work (TAPS = false)
+    stt.init();
     const PtLaunch &L = P.L;
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
     auto shade_one = [&](uint32_t i, const float4 &a, const float4 &b, const float4 &c, const uint4 &d,
@@ -193,6 +195,8 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         float dv0 = nd.x, dv1 = nd.y, dv2 = nd.z;
         int mat = int(d.z);
         if constexpr (!TAPS) {
+            // (the taps' counters go to their own half of the stats buffer:
+            // pt_dispatch_stats sums both, bench.py splits the flops by pass)
             // hit record: d.z/d.w = check[] bits 0..63, nd = {tap bound, material, check[] bits 64..127}
             const Check ck{uint64_t(d.z) | (uint64_t(d.w) << 32),
                            uint64_t(__float_as_uint(nd.z)) | (uint64_t(__float_as_uint(nd.w)) << 32)};
@@ -203,7 +207,9 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             for (int k = 0; k < 6; ++k) {
                 float qx, qy, qz;
                 map_point(ST_NORMAL, k, ro, rd, 0.0f, qx, qy, qz);
-                const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, bnd, st);
+                if constexpr (ST)
+                    if (first_active_lane()) stt.add(PT_ST_WAVE_MAPS);
+                const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, bnd, stt);
                 if ((k & 1) == 0) {
                     dp = h.d;  // d(p + e)
                 } else {
@@ -213,7 +219,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                     else dv2 = dd;
                 }
             }
-            st.add(PT_ST_NORMAL_MAPS, 6);
+            stt.add(PT_ST_NORMAL_MAPS, 6);
         }
         const bool done = shade_lane<ST>(L.mats, L.bounces, mat, dv0, dv1, dv2, 0, rng, ro, rd, thr, ret, seg, st);
         if (done) {
@@ -242,6 +248,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     }
     hist_flush(lh, P.hist);
     flush_stats<ST>(L, st);
+    if constexpr (!TAPS) flush_stats<ST>(L, stt, PT_ST_COUNT);
 }
 
 // scan: exclusive prefix of the histogram (one block of PT_BINS/4 threads);

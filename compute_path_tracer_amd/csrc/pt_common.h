@@ -269,13 +269,14 @@ struct InterpMap {
     }
 };
 
+// (base: PT_ST_COUNT for the second half, the shade pass's normal taps)
 template <bool ST>
-__device__ __forceinline__ void flush_stats(const PtLaunch &L, Stats<ST> &st) {
+__device__ __forceinline__ void flush_stats(const PtLaunch &L, Stats<ST> &st, int base = 0) {
     if constexpr (ST) {
         for (int k = 0; k < PT_ST_COUNT; ++k) {
             unsigned long long v = st.c[k];
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-            if ((threadIdx.x & 63) == 0) atomicAdd(&L.stats[k], v);
+            if ((threadIdx.x & 63) == 0) atomicAdd(&L.stats[base + k], v);
         }
     }
 }

@@ -51,7 +51,8 @@ struct pt_ctx {
     PtAabb *d_aabbs = nullptr;
     PtMat *d_mats = nullptr;
     size_t cap_nodes = 0, cap_aabbs = 0, cap_mats = 0;
-    unsigned long long *d_stats = nullptr;
+    unsigned long long *d_stats = nullptr;  // 2 x PT_ST_COUNT (second half: the shade pass's normal taps)
+    unsigned long long tap_stats[PT_ST_COUNT] = {};  // last pt_dispatch_stats: the shade-pass taps' share
     // tiles
     uint32_t rank = 0, nranks = 1;
     ncclComm_t comm = nullptr;
@@ -506,7 +507,7 @@ int pt_create(int hip_device, uint32_t width, uint32_t height, pt_ctx **out) {
     c->device = hip_device;
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->d_stats, sizeof(unsigned long long) * PT_ST_COUNT) != hipSuccess) {
+        hipMalloc(&c->d_stats, sizeof(unsigned long long) * 2 * PT_ST_COUNT) != hipSuccess) {
         pt_destroy(c);
         return PT_ERR_HIP;
     }
@@ -985,15 +986,16 @@ int pt_dispatch_stats(pt_ctx *c, const pt_constants *k, const pt_settings *s, ui
     if (rc != PT_OK) return rc;
     if (!counters) return fail(c, PT_ERR_INVALID, "null counters");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * PT_ST_COUNT, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 2 * PT_ST_COUNT, c->stream));
     L.stats = c->d_stats;
     L.write = 0;
     if (spp > 0 && L.n_tiles > 0)
         if ((rc = launch(c, L, true)) != PT_OK) return rc;
-    unsigned long long host[PT_ST_COUNT];
+    unsigned long long host[2 * PT_ST_COUNT];  // [0, COUNT): everything else; [COUNT, 2 COUNT): shade-pass taps
     HIPCHK(c, hipMemcpyAsync(host, c->d_stats, sizeof host, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; i < PT_STAT_COUNT; ++i) counters[i] = i < PT_ST_COUNT ? host[i] : 0;
+    for (int i = 0; i < PT_STAT_COUNT; ++i) counters[i] = i < PT_ST_COUNT ? host[i] + host[PT_ST_COUNT + i] : 0;
+    for (int i = 0; i < PT_ST_COUNT; ++i) c->tap_stats[i] = host[PT_ST_COUNT + i];
     return PT_OK;
 }
 
@@ -1194,6 +1196,11 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * double(c->n_lanes) * kBinBytesPerSample;
     else if (!std::strcmp(key, "bin_lanes")) *value = double(bin_lanes(c));
     else if (!std::strcmp(key, "shade_taps")) *value = shade_taps(c) ? 1.0 : 0.0;
+    else if (!std::strncmp(key, "tap_stat_", 9)) {  // tap_stat_<k>: counter k of the last stats run's shade-pass taps
+        const int k = std::atoi(key + 9);
+        if (k < 0 || k >= PT_ST_COUNT) return fail(c, PT_ERR_INVALID, "tap_stat index out of range");
+        *value = double(c->tap_stats[k]);
+    }
     else return fail(c, PT_ERR_INVALID, std::string("unknown option ") + key);
     return PT_OK;
 }

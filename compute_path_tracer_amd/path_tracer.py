@@ -126,6 +126,12 @@ class PathTracer:
                                                                   ctypes.byref(self.settings), spp, buf))
         return dict(zip(N.STAT_NAMES, (int(v) for v in buf)))
 
+    def tap_stats(self) -> dict:
+        """The share of the last stats() run done by the shade pass's normal
+        taps (shade_taps on; zeros otherwise)."""
+        return {name: int(self.get_option(f"tap_stat_{k}")) for k, name in enumerate(N.STAT_NAMES)
+                if k < N.PT_ST_COUNT}
+
     KERNELS = {"auto": 0, "simple": 1, "wave": 2, "jit": 2, "binned": 3}
 
     def set_option(self, key: str, value) -> None:

@@ -23,7 +23,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HOT = ("pt_bin_trace_jit", "pt_bin_trace_kernel", "pt_wave_jit", "pt_wave_kernel", "pt_render_kernel")
+HOT = ("pt_bin_trace_m_jit", "pt_bin_trace_jit", "pt_bin_trace_kernel", "pt_wave_jit", "pt_wave_kernel", "pt_render_kernel")
 
 
 def hot_name(name: str) -> bool:

@@ -249,6 +249,16 @@ def test_work_counters_match_oracle(gpu, kernel):
               "xform_shape", "sdf_sphere", "sdf_cube", "sdf_octahedron", "comb_union", "comb_sub", "comb_assign",
               "rr_break"):
         assert got[k] == ct[k], (k, got[k], ct[k])
+    # where the normal taps ran: the shade pass (scene kernels, shade_taps on)
+    # reports them in its own share, which bench.py keeps out of the trace
+    # pass's flops
+    taps = pt.tap_stats()
+    if KERNELS[kernel]["kernel"] == "binned" and KERNELS[kernel]["jit"] and pt.get_option("shade_taps") == 1.0:
+        assert taps["normal_maps"] == ct["normal_maps"] and taps["march_steps"] == 0
+        assert 0 < taps["xform_shape"] < got["xform_shape"]
+    else:
+        assert all(v == 0 for v in taps.values()), taps
+    pt.close()
 
 
 @pytest.mark.parametrize("name,spp", [("c3", 16), ("c2", 16)])
