@@ -201,6 +201,11 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             const Check ck{uint64_t(d.z) | (uint64_t(d.w) << 32),
                            uint64_t(__float_as_uint(nd.z)) | (uint64_t(__float_as_uint(nd.w)) << 32)};
             const float bnd = nd.x;
+            // bnd widened by the taps' spread (two taps are at most 2e apart,
+            // plus their coordinates' rounding): the first tap's tests against
+            // it leave in `live` every shape any tap may need
+            const float bndw = bnd + (0x1.a3ap-13f + 0x1p-20f * (fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z)));
+            uint64_t live = 0ull;
             mat = int(__float_as_uint(nd.y));
             float dp = 0.0f;
 #pragma unroll 1
@@ -209,7 +214,8 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                 map_point(ST_NORMAL, k, ro, rd, 0.0f, qx, qy, qz);
                 if constexpr (ST)
                     if (first_active_lane()) stt.add(PT_ST_WAVE_MAPS);
-                const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, bnd, stt);
+                const Hit h = k == 0 ? Map::template first<ST>(L, qx, qy, qz, ck, bnd, bndw, live, stt)
+                                     : Map::template rest<ST>(L, qx, qy, qz, ck, bnd, bndw, live, stt);
                 if ((k & 1) == 0) {
                     dp = h.d;  // d(p + e)
                 } else {
@@ -471,7 +477,8 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             if (mapping) {
                 float qx, qy, qz;
                 map_point(state, step, ro, rd, t, qx, qy, qz);
-                const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, __builtin_inff(), st);
+                uint64_t live = 0;  // (the taps' live mask: unused here)
+                const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, __builtin_inff(), __builtin_inff(), live, st);
                 after_map<ST>(h, state, step, t, ro, rd, mat, dv0, dv1, dv2, st);
                 if constexpr (!TAPS) {
                     if (state == ST_NORMAL) {  // hit: the shade pass takes the taps

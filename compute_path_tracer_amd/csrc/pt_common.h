@@ -211,7 +211,7 @@ __device__ __forceinline__ void count_eval(Stats<ST> &st) {
 struct InterpMap {
     template <bool ST>
     static __device__ Hit eval(const PtLaunch &L, float qx, float qy, float qz, const Check &ck, float /*bnd*/,
-                               Stats<ST> &st) {
+                               float /*bndw*/, uint64_t & /*live*/, Stats<ST> &st) {
         Hit cur{kMaxHit, 0};
         Hit s0{kMaxHit, 0};
         float px = qx, py = qy, pz = qz;
