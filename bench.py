@@ -114,7 +114,9 @@ def profiled_traffic(config: dict):
             continue
         cfg = d.get("bench_config") or {}
         keys = ("width", "height", "bounces", "spp_per_step")
-        if all(cfg.get(k) == config.get(k) for k in keys) and cfg.get("workload") == config.get("workload"):
+        same_lanes = cfg.get("pipelines", 2) == config.get("pipelines", 2)  # (older summaries: the default 2)
+        if all(cfg.get(k) == config.get(k) for k in keys) and cfg.get("workload") == config.get("workload") \
+                and same_lanes:
             hb = d.get("derived", {}).get("hbm_bytes_per_launch")
             if hb:
                 best = (hb, os.path.relpath(f, ROOT))
@@ -299,7 +301,8 @@ def main() -> None:
         "config": {"workload": f"{args.scene} {args.width}x{args.height}, {args.bounces} bounces, "
                                f"{args.spp * world} spp per step ({args.spp} per GPU-share), progressive accumulate",
                    "width": args.width, "height": args.height, "bounces": args.bounces,
-                   "spp_per_step": args.spp * world, "parallelism": f"tiles{world}"},
+                   "spp_per_step": args.spp * world, "parallelism": f"tiles{world}",
+                   "pipelines": int(pt.get_option("bin_lanes"))},
         "roofline": {"bound": "valu", "kernel": hot, "achieved": round(achieved_tf, 3), "peak": PEAK_F32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_TFLOPS, 4), "traffic": None,
                      "traffic_source": None,

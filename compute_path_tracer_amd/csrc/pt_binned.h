@@ -257,32 +257,47 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     if constexpr (!TAPS) flush_stats<ST>(L, stt, PT_ST_COUNT);
 }
 
-// scan: exclusive prefix of the histogram (one block of PT_BINS/4 threads);
-// clears the histogram and this pass's cursors.
+// scan: exclusive prefix of the histogram; clears the histogram and this
+// pass's cursors.  One wave (PT_SCAN_THREADS lanes, PT_BINS / 64 bins each,
+// no LDS): it fits on a CU beside the other pipeline's persistent trace
+// waves (28 of 32 slots), where a 1024-thread block waited for that trace
+// pass to drain (1.26 ms per launch with two pipelines, 5 us alone).
+#define PT_SCAN_THREADS 64
 __device__ __forceinline__ void bin_scan_body(const PtPass &P) {
-    __shared__ uint32_t part[PT_BINS / 4];
+    constexpr int PER = PT_BINS / PT_SCAN_THREADS;
     const int t = int(threadIdx.x);
-    uint32_t v[4], sum = 0u;
-    for (int j = 0; j < 4; ++j) {
-        v[j] = P.hist[t * 4 + j];
-        sum += v[j];
+    uint4 *h4 = reinterpret_cast<uint4 *>(P.hist + t * PER);
+    uint4 *o4 = reinterpret_cast<uint4 *>(P.offs + t * PER);
+    uint32_t sum = 0u;
+#pragma unroll
+    for (int j = 0; j < PER / 4; ++j) {
+        const uint4 v = h4[j];
+        sum += v.x + v.y + v.z + v.w;
     }
-    part[t] = sum;
-    __syncthreads();
-    for (int off = 1; off < PT_BINS / 4; off <<= 1) {
-        const uint32_t x = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += x;
-        __syncthreads();
+    uint32_t inc = sum;  // inclusive prefix over the wave's lanes
+#pragma unroll
+    for (int off = 1; off < PT_SCAN_THREADS; off <<= 1) {
+        const uint32_t x = uint32_t(__shfl_up(int(inc), off, PT_SCAN_THREADS));
+        if (t >= off) inc += x;
     }
-    uint32_t run = part[t] - sum;
-    for (int j = 0; j < 4; ++j) {
-        P.offs[t * 4 + j] = run;
-        run += v[j];
-        P.hist[t * 4 + j] = 0u;
+    uint32_t run = inc - sum;
+#pragma unroll
+    for (int j = 0; j < PER / 4; ++j) {
+        const uint4 v = h4[j];
+        uint4 o;
+        o.x = run;
+        run += v.x;
+        o.y = run;
+        run += v.y;
+        o.z = run;
+        run += v.z;
+        o.w = run;
+        run += v.w;
+        o4[j] = o;
+        h4[j] = make_uint4(0u, 0u, 0u, 0u);
     }
-    if (t == PT_BINS / 4 - 1) {
-        P.ctrl[0] = part[t];
+    if (t == PT_SCAN_THREADS - 1) {
+        P.ctrl[0] = inc;
         P.ctrl[1] = 0u;
     }
 }
