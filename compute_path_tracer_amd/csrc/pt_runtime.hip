@@ -771,10 +771,14 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         const int r = v ? std::atoi(v) : 4;
         return r >= 1 && r <= 64 ? r : 4;
     }();
-    static const unsigned shade_cu = [] {  // A/B knob: shade blocks per CU
+    static const unsigned shade_cu_env = [] {  // A/B knob: shade blocks per CU
         const char *v = std::getenv("PT_SHADE_BLOCKS");
-        return v ? unsigned(std::atoi(v)) : 8u;
+        return v ? unsigned(std::atoi(v)) : 0u;
     }();
+    // default: two rounds of the tapping shade kernel's 7 resident blocks per
+    // CU (measured +2 % over 8, whose last round ran on a quarter of the
+    // chip); 8 for the table kernel
+    const unsigned shade_cu = shade_cu_env ? shade_cu_env : (taps_shade ? 14u : 8u);
     const unsigned shade_grid =
         unsigned(std::max<size_t>(1, std::min<size_t>((c->bin_cap + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK, size_t(shade_cu) * cu)));
 
