@@ -104,6 +104,17 @@ __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro,
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// bounds() of the shade pass, per map type: the generic box loop; the
+// scene kernels specialise it (pt_jit.cpp: straight-line slab tests with
+// constant check[] bits, boxes baked as literals in the tier-up build).
+template <class Map>
+struct MapBounds {
+    template <bool ST>
+    static __device__ __forceinline__ uint4 mask(const PtLaunch &L, const pt_f3 &ro, const pt_f3 &rd, Stats<ST> &st) {
+        return bounds_mask<ST>(L, ro, rd, st);
+    }
+};
+
 __device__ __forceinline__ void store_ray(PtRay *r, const pt_f3 &ro, const pt_f3 &rd, const pt_f3 &thr,
                                           const pt_f3 &ret, uint32_t rng, uint32_t sid, uint32_t m0, uint32_t m1) {
     float4 *v = reinterpret_cast<float4 *>(r);
@@ -234,7 +245,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             P.key[i] = PT_BIN_NONE;
             return;
         }
-        const uint4 m = bounds_mask<ST>(L, ro, rd, st);
+        const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
         store_ray(P.rin + i, ro, rd, thr, ret, rng, d.y, m.x, m.y);
         if (P.wide) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);

@@ -43,7 +43,8 @@ struct PtJitModule {
 // in the node table, value-only edits do not recompile); bake=true: node
 // values become exact f32 literals too (no scalar loads; recompiles, cached,
 // when a value changes).
-std::string pt_jit_source(const std::vector<PtNode> &nodes, bool bake);
+std::string pt_jit_source(const std::vector<PtNode> &nodes, const std::vector<PtAabb> &boxes, bool fast_bounds,
+                          bool bake);
 // Compile with hipRTC for gfx950; returns the code object or an error log.
 bool pt_jit_compile_source(const std::string &src, std::vector<char> &code, std::string &log);
 // Load a code object on the current device.

@@ -203,7 +203,7 @@ bool jit_wanted(const pt_ctx *c) {
 
 // (Re)build the scene-specialised kernel when the generated source changed.
 // A failure leaves the interpreter kernel in use and records the log.
-void jit_refresh(pt_ctx *c, const std::vector<PtNode> &nodes) {
+void jit_refresh(pt_ctx *c, const std::vector<PtNode> &nodes, const std::vector<PtAabb> &boxes) {
     if (!jit_wanted(c)) {
         pt_jit_unload(c->jit_mod);
         pt_jit_unload(c->jit_tier);
@@ -211,9 +211,9 @@ void jit_refresh(pt_ctx *c, const std::vector<PtNode> &nodes) {
         return;
     }
     const int bake = jit_bake(c);
-    std::string src = pt_jit_source(nodes, bake == 1);
+    std::string src = pt_jit_source(nodes, boxes, c->fast_bounds, bake == 1);
     // the tier-up build for these values (jit_bake 2); a stale one is dropped
-    c->tier_want = bake == 2 ? pt_jit_source(nodes, true) : std::string();
+    c->tier_want = bake == 2 ? pt_jit_source(nodes, boxes, c->fast_bounds, true) : std::string();
     if (c->jit_tier.module && c->jit_tier.key != c->tier_want) pt_jit_unload(c->jit_tier);
     if (!(c->jit_mod.module && c->jit_mod.key == src)) {
         pt_jit_unload(c->jit_mod);
@@ -598,7 +598,7 @@ int pt_set_data(pt_ctx *c, const float *data, uint32_t n) {
     for (const PtAabb &b : boxes)
         for (int k = 0; k < 3; ++k)
             if (!pt_div_coord_ok(b.bmin[k]) || !pt_div_coord_ok(b.bmax[k])) c->fast_bounds = false;
-    jit_refresh(c, nodes);
+    jit_refresh(c, nodes, boxes);
     return PT_OK;
 }
 
