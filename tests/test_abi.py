@@ -52,8 +52,13 @@ def test_null_and_state_errors_without_device():
         assert rc == N.PT_ERR_HIP and not ctx.value
 
 
+@pytest.mark.parametrize("bake", ["0", "1"])
 @pytest.mark.parametrize("name", ["c2", "c3"])
-def test_scene_kernel_builds_with_hiprtc(name):
+def test_scene_kernel_builds_with_hiprtc(name, bake, monkeypatch):
+    # table and values-baked builds (the baked one also bakes the bounds()
+    # boxes); the 124-entry "wide" scene (all four mask words) compiles in
+    # the GPU parity tests, too slowly for this suite (~75 s)
+    monkeypatch.setenv("PT_JIT_BAKE", bake)
     L = N.lib()
     prog = scenes.SCENES[name]().compile(CompData())
     log = ctypes.create_string_buffer(1 << 16)
