@@ -72,6 +72,32 @@ def algorithmic_flops(st: dict) -> float:
     return float(f)
 
 
+def pipeline_bytes(st: dict, pixels: float) -> dict:
+    """Algorithmic HBM bytes of one dispatch of the binned pipeline
+    (pt_binned.h), from the instrumented run's counters: S samples, G
+    segments (rays entering a trace pass), H shaded hits.  Misses G - H end
+    in the trace pass; G - S rays continue from a shade pass; H - (G - S)
+    paths end there.  Per pass and ray: gen writes the 64 B ray + 4 B key;
+    scatter reads every slot's 4 B key and writes a 4 B binned slot; trace
+    reads a slot (4 B) and its ray (64 B) and writes a colour + end marker
+    (16 + 4 B, miss) or a hit record + tap record + marker (64 + 16 + 4 B);
+    shade reads each slot's marker (4 B) and each hit's 64 + 16 B and writes
+    the next ray + key (64 + 4 B) or the colour + marker (16 + 4 B); fold
+    reads each frame's colour (16 B) and reads + writes the texel (32 B per
+    pixel).  Scenes with > 64 check[] entries add 8 B per ray move (not
+    counted here: the bench scene has 24)."""
+    S, G, H = float(st["samples"]), float(st["segments"]), float(st["shaded"])
+    cont, miss = G - S, G - H
+    ended = H - cont
+    parts = {"gen": 68.0 * S,
+             "scatter": 8.0 * G,
+             "trace": 68.0 * G + 20.0 * miss + 84.0 * H,
+             "shade": 4.0 * G + 80.0 * H + 68.0 * cont + 20.0 * ended,
+             "fold": 16.0 * S + 32.0 * pixels}
+    parts["total"] = sum(parts.values())
+    return parts
+
+
 def schedule_metrics(st_all: dict, taps: dict) -> dict:
     """SIMD efficiency of the wavefront schedule from the instrumented run:
     the trace passes (st_all minus the shade pass's normal taps), and the
@@ -270,7 +296,8 @@ def main() -> None:
     d_ms = float(np.mean(kernel_ms))  # one dispatch = one step's frames of this rank
     flops_step = algorithmic_flops(st)
     rank_pixels = st["samples"] / max(1, spp_step)
-    bytes_per_launch = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per dispatch
+    image_bytes = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per dispatch
+    pipe = pipeline_bytes(st, rank_pixels)
     jit = bool(pt.get_option("jit_active"))
     shade_taps = bool(pt.get_option("shade_taps")) and jit
     if trace_n:  # dominant kernel: the binned trace pass (flops of its passes / their device time)
@@ -284,7 +311,7 @@ def main() -> None:
         launches, t_ms, k_ms = 1.0, d_ms, d_ms
         achieved_tf = flops_step / (d_ms * 1e-3) / 1e12
     path_tf = flops_step / (d_ms * 1e-3) / 1e12
-    achieved_gbs = bytes_per_launch / (d_ms * 1e-3) / 1e9
+    achieved_gbs = pipe["total"] / (d_ms * 1e-3) / 1e9  # whole dispatch: every pass's algorithmic bytes
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -314,7 +341,13 @@ def main() -> None:
                      "dispatch_ms_per_step": round(d_ms, 3),
                      "path_achieved": round(path_tf, 3), "path_frac": round(path_tf / PEAK_F32_TFLOPS, 4)},
         "hbm": {"achieved": round(achieved_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved_gbs / PEAK_HBM_GBS, 6), "algorithmic_bytes_per_launch": bytes_per_launch},
+                "frac": round(achieved_gbs / PEAK_HBM_GBS, 6),
+                "scope": "binned pipeline's algorithmic bytes per dispatch (all passes) / dispatch time",
+                "algorithmic_bytes_per_dispatch": pipe["total"],
+                "bytes_per_sample": round(pipe["total"] / max(1, st["samples"]), 1),
+                "by_pass": {k: v for k, v in pipe.items() if k != "total"},
+                "image_bytes_per_dispatch": image_bytes,
+                "image_gbs": round(image_bytes / (d_ms * 1e-3) / 1e9, 3)},
         "work": st,
         "schedule": schedule_metrics(st, taps),
         "jit": {"active": jit, "compile_s": round(pt.get_option("jit_seconds"), 3),
@@ -336,7 +369,7 @@ def main() -> None:
     if tr_prof is not None:
         out["roofline"]["traffic"] = tr_prof[0]
         out["roofline"]["traffic_source"] = f"{tr_prof[1]} (2*FETCH_SIZE+WRITE_SIZE, KiB->B, per launch)"
-        out["hbm"]["measured_bytes_per_launch"] = tr_prof[0]
+        out["hbm"]["trace_kernel_measured_bytes_per_launch"] = tr_prof[0]
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(ed, args.width, args.height, args.bounces, args.cpu_threads,
                                            args.cpu_row_stride, args.cpu_spp)

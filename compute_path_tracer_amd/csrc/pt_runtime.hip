@@ -74,7 +74,9 @@ struct pt_ctx {
     std::string tier_want;  // baked source for the current values
     std::string tier_job_src;
     std::string tier_failed;  // a baked source that did not build (not retried)
-    std::future<std::vector<char>> tier_job;  // code object (empty: compile failed)
+    // code object (empty: compile failed) and its compile seconds; the worker
+    // returns both through the future, so no field is shared with it
+    std::future<std::pair<std::vector<char>, double>> tier_job;
     double tier_seconds = 0.0;
     // binned pipeline buffers (pt_binned.h).  A chunk's frames are split over
     // up to kMaxLanes independent pipelines ("lanes"), each on its own stream,
@@ -160,7 +162,9 @@ std::vector<char> jit_code(const std::string &src, std::string &log, double *sec
 void jit_tier_poll(pt_ctx *c, bool wait) {
     if (c->tier_job.valid() &&
         (wait || c->tier_job.wait_for(std::chrono::seconds(0)) == std::future_status::ready)) {
-        std::vector<char> code = c->tier_job.get();
+        auto done = c->tier_job.get();
+        std::vector<char> &code = done.first;
+        c->tier_seconds = done.second;
         if (code.empty()) c->tier_failed = c->tier_job_src;
         if (!code.empty() && c->tier_job_src == c->tier_want && !c->jit_tier.module) {
             std::string err;
@@ -177,10 +181,11 @@ void jit_tier_poll(pt_ctx *c, bool wait) {
         c->tier_want != c->tier_failed) {
         std::string src = c->tier_want;
         c->tier_job_src = src;
-        double *secs = &c->tier_seconds;
-        c->tier_job = std::async(std::launch::async, [src, secs]() {
+        c->tier_job = std::async(std::launch::async, [src]() {
             std::string log;
-            return jit_code(src, log, secs);
+            double secs = 0.0;
+            std::vector<char> code = jit_code(src, log, &secs);
+            return std::make_pair(std::move(code), secs);
         });
         if (wait) jit_tier_poll(c, true);
     }

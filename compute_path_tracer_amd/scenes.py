@@ -263,6 +263,52 @@ def cull_stress(seed: int = 11) -> SDFEditor:
     return ed
 
 
+def tiny_union() -> SDFEditor:
+    """Open space towards a distant backdrop, with two specks behind the
+    camera: header unions of scale 1e-3 and 2e-3 whose shapes are ~1 unit in
+    their own frame.  A union returns MAXHIT * s (= 10,
+    20 world units) when none of its shapes combines, so rays through open
+    space (parent distance > 10) check that the scene kernels' distance-bound
+    culling of a union's first (assign) shape keeps the reference's value
+    (containers.rs:244-252: u = shape overwrites MAXHIT)."""
+    a = _union("anchor")
+    lamp = _shape(Shapes.SPHERE, pos=(0.0, -0.2, 2.0), size=(0.6,), name="lamp")
+    _mat(lamp, col=(0.9, 0.8, 0.7), brightness=2.0)
+    box = _shape(Shapes.CUBE, pos=(1.2, 0.4, 3.0), rot=(0.3, 0.5, 0.0), size=(0.3, 0.3, 0.3), name="box")
+    _mat(box, col=(0.3, 0.6, 0.9), spec=0.5, rough=0.2)
+    wall = _shape(Shapes.CUBE, pos=(0.0, 0.0, 40.0), size=(80.0, 80.0, 1.0), aabb=False, name="backdrop")
+    _mat(wall, col=(0.7, 0.7, 0.7), brightness=0.5)
+    a.children_shapes += [lamp, box, wall]
+    # behind the camera: farther than the running distance while rays cross
+    # the open space towards the backdrop, so their shapes are dropped
+    sp = _union("speck-a", pos=(0.4, 0.3, -20.0), rot=(0.2, 0.1, 0.4), scale=1e-3)
+    for k, (kind, pos, size, aabb) in enumerate([(Shapes.SPHERE, (0, 0, 0), (1.0,), False),
+                                                 (Shapes.CUBE, (1.5, 0, 0), (0.8, 0.8, 0.8), False),
+                                                 (Shapes.SPHERE, (0, 1.5, 0), (0.5,), True)]):
+        s = _shape(kind, pos=pos, size=size, aabb=aabb, name=f"speck-a-{k}")
+        _mat(s, col=(0.8, 0.2, 0.2), brightness=5.0)
+        sp.children_shapes.append(s)
+    sb = _union("speck-b", pos=(-0.5, 0.2, -25.0), scale=2e-3)
+    s = _shape(Shapes.CUBE, size=(1.0, 1.0, 1.0), aabb=False, name="speck-b-0")
+    _mat(s, col=(0.2, 0.8, 0.2))
+    sb.children_shapes.append(s)
+    return SDFEditor([a, sp, sb])
+
+
+def far_box() -> SDFEditor:
+    """c2 plus a sphere 1e20 units away with its AABB on: one box coordinate
+    outside the reciprocal-division guard, so every ray of
+    the scene takes bounds()'s IEEE-division path (scene kernels: the baked
+    'false' branch and the table kernel's fast_bounds = 0)."""
+    ed = c2_sphere_box_torus()
+    u = _union("far")
+    s = _shape(Shapes.SPHERE, pos=(1e20, 0.0, 0.0), size=(1.0,), name="far")
+    _mat(s, col=(0.5, 0.5, 0.5))
+    u.children_shapes.append(s)
+    ed.header_unions.append(u)
+    return ed
+
+
 _DEPRECATED_KINDS = {"Sphere": Shapes.SPHERE, "Cube": Shapes.CUBE, "OctahedronExact": Shapes.OCTAHEDRON}
 
 
@@ -320,6 +366,8 @@ SCENES = {
     "c3_noaabb": c3_no_aabb,
     "wide": wide_graph,
     "cull": cull_stress,
+    "tiny": tiny_union,
+    "farbox": far_box,
 }
 
 # BASELINE.json configs -> (scene, width, height, spp, bounces)

@@ -161,3 +161,36 @@ def test_cull_scene_switches_the_rule_off_where_values_demand(tmp_path):
     assert all(math.isfinite(p) for k, p in enumerate(pads) if k not in (2, 7, 8))
     neg = [n for n in nodes if n["op"] == N.PT_OP_SHAPE and n["shape"] == N.PT_NODE_SPHERE and n["size"][0] < 0]
     assert neg and all(math.isfinite(n["pad"]) for n in neg)  # R = r < 0 still bounds a sphere
+
+
+def test_dropped_assign_shape_stands_in_as_inf(tmp_path):
+    """A union's first shape is combined by assignment (containers.rs:244-252),
+    which overwrites MAXHIT.  When the cull drops it, the scene kernel must not
+    leave MAXHIT * s (10 world units at scale 1e-3, which would beat a larger
+    parent distance): it assigns +inf, a value above the cull target as the
+    dropped shape's own was.  The speck unions of scene "tiny" are cull-eligible."""
+    src, nodes = _baked("tiny", tmp_path)
+    begins = [i for i, n in enumerate(nodes) if n["op"] == N.PT_OP_UNION_BEGIN]
+    assert len(begins) == 3 and all(math.isfinite(nodes[i]["pad"]) for i in begins[1:])
+    for b in begins[1:]:
+        first = b + 1
+        assert nodes[first]["combine"] == N.PT_COMBINE_ASSIGN
+        mat_tag = f"h1 = Hit{{__builtin_inff(), "
+        body = src[src.index(f"// shape {first}\n"):]
+        body = body[:body.index("    }\n")]
+        assert "if (cut) " + mat_tag in body, body
+    # JitMapB1's whole-union skip (live mask) assigns +inf too
+    b1 = src[src.index("struct JitMapB1"):]
+    assert b1.count("} else {  // live") >= 1
+    live = b1[b1.index("} else {  // live"):]
+    assert live[:live.index("if constexpr")].count("= Hit{__builtin_inff(), ") == 1
+
+
+def test_far_box_takes_the_ieee_bounds_path(tmp_path):
+    """A box coordinate beyond the reciprocal guard (scene "farbox", 1e20)
+    makes the values-baked shade kernel's bounds() select its IEEE-division
+    branch for every ray; the GPU parity test runs it."""
+    src, _ = _baked("farbox", tmp_path)
+    assert "const bool fast = false && " in src
+    src_c2, _ = _baked("c2", tmp_path)
+    assert "const bool fast = true && " in src_c2

@@ -78,6 +78,8 @@ def _report(gpu, ref):
     ("wide", 48, 32, 2, 6),        # 124 check[] entries: the high mask words
     ("c3_noaabb", 40, 24, 2, 8),   # no bounds() boxes: every mask empty, one bin
     ("cull", 64, 40, 3, 6),        # distance-bound culling near its threshold, rule on/off per union
+    ("tiny", 64, 40, 3, 4),        # unions of scale 1e-3: culled first shapes in open space (MAXHIT * s = 10)
+    ("farbox", 64, 40, 3, 4),      # a box coordinate beyond the reciprocal guard: IEEE-division bounds()
 ])
 def test_parity_path_trace(gpu, name, w, h, spp, bounces, kernel):
     gpu_img, ref = _render_pair(scenes.SCENES[name](), w, h, spp, bounces, kernel=kernel)
