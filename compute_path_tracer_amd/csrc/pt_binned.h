@@ -440,6 +440,16 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             const int src = int(wtake) + r;
             const bool got = state == ST_FREE && uint32_t(r) < take;
             if (!in_lds) {  // first refill from this window: park it in LDS (waits for its loads)
+                // the wave's check[] union (Check.alo/ahi) for the scene kernels:
+                // the masks of the lanes still mapping and of the whole window,
+                // so it also covers every lane this window's refills start
+                const bool mapping_now = state == ST_MARCH || state == ST_NORMAL;
+                const bool in_win = uint32_t(lane) < wcnt;
+                ck.alo = wave_or_u64((mapping_now ? ck.lo : 0ull) |
+                                     (in_win ? (uint64_t(s3.z) | (uint64_t(s3.w) << 32)) : 0ull));
+                ck.ahi = P.wide ? wave_or_u64((mapping_now ? ck.hi : 0ull) |
+                                              (in_win ? (uint64_t(sh.x) | (uint64_t(sh.y) << 32)) : 0ull))
+                                : 0ull;
                 W[0][lane] = make_uint4(__float_as_uint(s0.x), __float_as_uint(s0.y), __float_as_uint(s0.z),
                                         __float_as_uint(s0.w));
                 W[1][lane] = make_uint4(__float_as_uint(s1.x), __float_as_uint(s1.y), __float_as_uint(s1.z),

@@ -35,7 +35,19 @@ struct Hit {
 
 struct Check {  // check[] of the generated bounds(), one bit per entry
     uint64_t lo, hi;
+    // a superset of the check[] bits of every lane of the wave that maps with
+    // this mask, wave-uniform (scene kernels test it first: a shape no lane
+    // needs is skipped by a scalar branch); all ones = no information
+    uint64_t alo = ~0ull, ahi = ~0ull;
 };
+// a lane's check[] bit behind the wave-uniform test of Check.alo/ahi: the
+// empty volatile asm keeps the compiler from merging the two tests into one
+// vector test (it may not speculate a block with side effects), so the
+// uniform one stays a scalar branch
+__device__ __forceinline__ bool lane_check(uint64_t m, int k) {
+    __asm__ volatile("");
+    return ((m >> k) & 1ull) != 0;
+}
 __device__ __forceinline__ bool check_bit(const Check &c, int k) {
     return k < 64 ? ((c.lo >> k) & 1ull) != 0 : ((c.hi >> (k - 64)) & 1ull) != 0;
 }
@@ -65,6 +77,22 @@ struct Stats {
         return 0;
     }
 };
+
+// OR of v over the 64 lanes of the wave (every lane active), wave-uniform:
+// an inclusive row scan by DPP row shifts, then the rows' totals by row
+// broadcasts; lane 63 holds the OR of all 64 lanes
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, false));  // row_shr:1
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, false));  // row_shr:2
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, false));  // row_shr:4
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, false));  // row_shr:8
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false));  // row_bcast:15 -> rows 1, 3
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false));  // row_bcast:31 -> rows 2, 3
+    return uint32_t(__builtin_amdgcn_readlane(int(v), 63));
+}
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
+    return uint64_t(wave_or_u32(uint32_t(v))) | (uint64_t(wave_or_u32(uint32_t(v >> 32))) << 32);
+}
 
 __device__ __forceinline__ int lane_rank(uint64_t m) {  // set bits of m below this lane
     return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
