@@ -88,10 +88,23 @@ __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro,
                       pt_div_coord_ok(ro.z) && pt_div_dir_ok(rd.x) && pt_div_dir_ok(rd.y) && pt_div_dir_ok(rd.z);
     if (fast) {
         const float yx = 1.0f / rd.x, yy = 1.0f / rd.y, yz = 1.0f / rd.z;
+        // slab values from the reciprocal products; a wave with an undecided
+        // comparison redoes every box exactly (ray_box_approx)
+        float gap = __builtin_inff();
 #pragma unroll 4  // scalar box loads issued ahead of their slab tests
         for (int b = 0; b < L.n_aabb; ++b) {
             const PtAabb bx = boxes[b];
-            if (ray_box_rcp(bx, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, yx, yy, yz)) w[bx.back >> 5] |= 1u << (bx.back & 31);
+            if (ray_box_approx(bx, ro.x, ro.y, ro.z, yx, yy, yz, gap)) w[bx.back >> 5] |= 1u << (bx.back & 31);
+        }
+        if (__builtin_expect(__ballot(!(gap > 0.0f)) != 0ull, 0)) {
+            uint32_t v[4] = {0u, 0u, 0u, 0u};
+            for (int b = 0; b < L.n_aabb; ++b) {
+                const PtAabb bx = boxes[b];
+                if (ray_box_rcp(bx, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, yx, yy, yz))
+                    v[bx.back >> 5] |= 1u << (bx.back & 31);
+            }
+            if (!(gap > 0.0f))
+                for (int k = 0; k < 4; ++k) w[k] = v[k];
         }
     } else {
         for (int b = 0; b < L.n_aabb; ++b) {
@@ -423,7 +436,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     uint32_t rng = 0u, sid = 0u, pos = 0u;
     pt_f3 ro{0.0f, 0.0f, 0.0f}, rd{0.0f, 0.0f, 1.0f};
     pt_f3 thr{1.0f, 1.0f, 1.0f}, ret{0.0f, 0.0f, 0.0f};
-    int seg = 0, step = 0, mat = 0;
+    int step = 0, mat = 0;  // (a lane's segment index is this pass's P.bounce)
     float t = 0.0f;
     float dv0 = 0.0f, dv1 = 0.0f, dv2 = 0.0f;
     Check ck{0ull, 0ull};
@@ -443,7 +456,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 // the wave's check[] union (Check.alo/ahi) for the scene kernels:
                 // the masks of the lanes still mapping and of the whole window,
                 // so it also covers every lane this window's refills start
-                const bool mapping_now = state == ST_MARCH || state == ST_NORMAL;
+                const bool mapping_now = state == ST_MARCH || (TAPS && state == ST_NORMAL);
                 const bool in_win = uint32_t(lane) < wcnt;
                 ck.alo = wave_or_u64((mapping_now ? ck.lo : 0ull) |
                                      (in_win ? (uint64_t(s3.z) | (uint64_t(s3.w) << 32)) : 0ull));
@@ -491,7 +504,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 ck.lo = uint64_t(d2) | (uint64_t(d3) << 32);
                 ck.hi = uint64_t(e0) | (uint64_t(e1) << 32);
                 pos = wbase + uint32_t(src);
-                seg = P.bounce;
                 t = 0.0f;
                 step = 0;
                 state = ST_MARCH;
@@ -503,7 +515,8 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         tm = st.lap(PT_ST_CYC_REFILL, tm);
 
         // ---- 2. one map() per marching / normal-tap lane ------------------
-        const bool mapping = state == ST_MARCH || state == ST_NORMAL;
+        // (TAPS = false: no lane is ever NORMAL here, the shade pass taps)
+        const bool mapping = state == ST_MARCH || (TAPS && state == ST_NORMAL);
         st.add(PT_ST_LANE_IDLE, mapping ? 0u : 1u);
         st.add(PT_ST_IDLE_SHADE, state == ST_SHADE ? 1u : 0u);
         st.add(PT_ST_IDLE_FREE, state == ST_FREE ? 1u : 0u);
@@ -512,10 +525,10 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             if (lane == 0) st.add(PT_ST_WAVE_MAPS);
             if (mapping) {
                 float qx, qy, qz;
-                map_point(state, step, ro, rd, t, qx, qy, qz);
+                map_point(TAPS ? state : int(ST_MARCH), step, ro, rd, t, qx, qy, qz);
                 uint64_t live = 0;  // (the taps' live mask: unused here)
                 const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, __builtin_inff(), __builtin_inff(), live, st);
-                after_map<ST>(h, state, step, t, ro, rd, mat, dv0, dv1, dv2, st);
+                after_map<ST, !TAPS>(h, state, step, t, ro, rd, mat, dv0, dv1, dv2, st);
                 if constexpr (!TAPS) {
                     if (state == ST_NORMAL) {  // hit: the shade pass takes the taps
                         dv0 = tap_bound(h.d, qx, qy, qz, t, L.bound_k);
@@ -530,7 +543,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         // is final), a hit goes to the shade pass with its normal differences
         if (state == ST_SHADE) {
             if (step < 0) {
-                const pt_f3 c = final_color(L.debug, seg, L.bounces, ret);
+                const pt_f3 c = final_color(L.debug, P.bounce, L.bounces, ret);
                 P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
                 P.key[pos] = PT_BIN_NONE;
             } else {

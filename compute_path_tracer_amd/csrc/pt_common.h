@@ -145,8 +145,24 @@ __device__ __forceinline__ void xform(const PtNode &n, float &x, float &y, float
 
 // sdCube (shapes.glsl:5-9) from q = abs(p) - b and qm = max(q): the
 // bound-culled scene map computes q first for its test.
+//
+// FAST (scene kernels, cubes whose faces are large next to the scene): when
+// at most one of mx, my, mz is nonzero (their median is 0) and that one, m,
+// is 0 or in [2^-60, 2^60], the sum of squares is RN(m^2) (the other terms
+// are +0) and sqrt(RN(m^2)) = m exactly (binary RN; checked for every
+// significand), so length(max(q, 0)) = m without the squares and the sqrt.
+// A wave takes that path when all its active lanes qualify.
+template <bool FAST = false>
 __device__ __forceinline__ float cube_from_q(float qx, float qy, float qz, float qm) {
     const float mx = pt_gmax(qx, 0.0f), my = pt_gmax(qy, 0.0f), mz = pt_gmax(qz, 0.0f);
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    if constexpr (FAST) {
+        const float m = pt_gmax(mx, pt_gmax(my, mz));
+        const bool easy = __builtin_amdgcn_fmed3f(mx, my, mz) == 0.0f &&
+                          (m == 0.0f || __builtin_amdgcn_fmed3f(m, 0x1p-60f, 0x1p60f) == m);
+        if (__ballot(!easy) == 0ull) return m + pt_gmin(qm, 0.0f);
+    }
+#endif
     return pt_sqrt(mx * mx + my * my + mz * mz) + pt_gmin(qm, 0.0f);
 }
 
@@ -155,13 +171,13 @@ __device__ __forceinline__ float cube_from_q(float qx, float qy, float qz, float
 __device__ __forceinline__ float cull_target(float a, float b) { return b < a ? b : a; }
 
 // SDFs, shapes.glsl:1-25 (+ torus extension)
-template <int K>
+template <int K, bool FASTCUBE = false>
 __device__ __forceinline__ float sdf_k(const PtNode &n, float x, float y, float z) {
     if constexpr (K == PT_NODE_SPHERE) {
         return pt_sqrt(x * x + y * y + z * z) - n.size[0];
     } else if constexpr (K == PT_NODE_CUBE) {
         const float qx = fabsf(x) - n.size[0], qy = fabsf(y) - n.size[1], qz = fabsf(z) - n.size[2];
-        return cube_from_q(qx, qy, qz, pt_gmax(qx, pt_gmax(qy, qz)));
+        return cube_from_q<FASTCUBE>(qx, qy, qz, pt_gmax(qx, pt_gmax(qy, qz)));
     } else if constexpr (K == PT_NODE_TORUS) {
         const float qx = pt_sqrt(x * x + z * z) - n.size[0];
         return pt_sqrt(qx * qx + y * y) - n.size[1];

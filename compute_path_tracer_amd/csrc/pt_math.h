@@ -98,14 +98,21 @@ PT_HD void pt_sincos(float x, float &s, float &c) {
 PT_HD float pt_sqrt(float x) {
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
     // x in [2^-96, 2^128) as an unsigned range test on the bits; anything else
-    // (zeros, negatives, tiny, inf, NaN) takes the IEEE sqrtf for the wave
+    // (zeros, negatives, tiny, inf, NaN) takes the IEEE sqrtf for the wave.
+    // The fast result is formed first and replaced afterwards (one rarely
+    // taken branch, no flow block around the common path).
+#ifdef PT_EXP_SQRT_OLD  // A/B (PT_JIT_DEFS): range test first, as before
     if (__builtin_expect(__ballot((__float_as_uint(x) - 0x0F800000u) >= (0x7F800000u - 0x0F800000u)) != 0ull, 0))
         return sqrtf(x);
+#endif
     const float y = __builtin_amdgcn_rsqf(x);
     const float g = x * y;
     const float h = 0.5f * y;
     const float r = fmaf(-g, g, x);
-    return fmaf(r, h, g);
+    float s = fmaf(r, h, g);
+    if (__builtin_expect(__ballot((__float_as_uint(x) - 0x0F800000u) >= (0x7F800000u - 0x0F800000u)) != 0ull, 0))
+        s = sqrtf(x);
+    return s;
 #else
     return sqrtf(x);
 #endif

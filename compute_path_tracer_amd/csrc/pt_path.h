@@ -52,6 +52,26 @@ __device__ __forceinline__ bool ray_box_rcp(const PtAabb &bx, float ox, float oy
     return tnear < tfar && tfar > 0.0f;
 }
 
+// The slab test from the reciprocal products alone: t' = RN(a * y) with a =
+// RN(bmin - o) as in ray_box_rcp and y = RN(1/d).  Under the same guards,
+// |t' - t| <= 3 * 2^-24 |t| for every slab value t = RN(a / d), and t' has
+// t's sign and zeros, so:
+//  * tfar' > 0 exactly when tfar > 0 (min / max keep the signs);
+//  * tnear < tfar is decided by tnear' < tfar' whenever |tfar' - tnear'| >
+//    2^-20 (|tnear'| + |tfar'|) (min / max move each end by <= 2^-22 of
+//    itself); `gap` keeps the least |tfar' - tnear'| - that margin over the
+//    boxes tested, and a lane whose gap is <= 0 takes ray_box_rcp.
+__device__ __forceinline__ bool ray_box_approx(const PtAabb &bx, float ox, float oy, float oz, float yx, float yy,
+                                               float yz, float &gap) {
+    const float tminx = (bx.bmin[0] - ox) * yx, tmaxx = (bx.bmax[0] - ox) * yx;
+    const float tminy = (bx.bmin[1] - oy) * yy, tmaxy = (bx.bmax[1] - oy) * yy;
+    const float tminz = (bx.bmin[2] - oz) * yz, tmaxz = (bx.bmax[2] - oz) * yz;
+    const float tnear = pt_gmax(pt_gmax(pt_gmin(tminx, tmaxx), pt_gmin(tminy, tmaxy)), pt_gmin(tminz, tmaxz));
+    const float tfar = pt_gmin(pt_gmin(pt_gmax(tminx, tmaxx), pt_gmax(tminy, tmaxy)), pt_gmax(tminz, tmaxz));
+    gap = fminf(gap, fabsf(tfar - tnear) - (fabsf(tnear) + fabsf(tfar)) * 0x1p-20f);
+    return tnear < tfar && tfar > 0.0f;
+}
+
 // The map() argument of a lane: CastRay's p = ro + rd*t (MARCH), or normal
 // tap `step` (0..5 = +x,-x,+y,-y,+z,-z) around the hit point held in ro
 // (calc_normal, test_compute.glsl:57-66).
@@ -76,10 +96,12 @@ __device__ __forceinline__ void map_point(int state, int step, const pt_f3 &ro, 
 // body and exit tests (test_compute.glsl:42-54); on exit either a miss
 // (-> SHADE with step = -1) or calc_point into ro (-> NORMAL).  NORMAL: the
 // six taps give the central differences d(p+e) - d(p-e) per axis.
-template <bool ST>
+// MARCH_ONLY: the caller never maps a NORMAL lane (the binned trace pass
+// whose shade pass takes the taps), so the taps' branch is left out.
+template <bool ST, bool MARCH_ONLY = false>
 __device__ __forceinline__ void after_map(const Hit &h, int &state, int &step, float &t, pt_f3 &ro, const pt_f3 &rd,
                                           int &mat, float &dv0, float &dv1, float &dv2, Stats<ST> &st) {
-    if (state == ST_MARCH) {
+    if (MARCH_ONLY || state == ST_MARCH) {
         st.add(PT_ST_MARCH);
         mat = h.m;
         t += h.d;
@@ -94,7 +116,7 @@ __device__ __forceinline__ void after_map(const Hit &h, int &state, int &step, f
                 step = 0;
             }
         }
-    } else {
+    } else if constexpr (!MARCH_ONLY) {
         if ((step & 1) == 0) {
             t = h.d;  // d(p + e)
         } else {

@@ -10,7 +10,7 @@
 #include <algorithm>
 
 #include "../../include/pt_abi.h"
-#include "pt_math.h"
+#include "pt_path.h"
 
 namespace {
 
@@ -117,7 +117,79 @@ __global__ void div_random(uint32_t seed, uint32_t n, unsigned long long *bad, u
     }
 }
 
+// The margin-decided slab test (pt_path.h ray_box_approx):
+// random guarded (box, ray) pairs; mode 1 puts the ray through a box edge
+// (entry and exit faces meet at one point, +-a few ulps), the near-ties the
+// margin must leave undecided.  Counts: [0] decided lanes whose answer differs
+// from the IEEE slab test, [1] undecided lanes whose exact answer
+// (ray_box_rcp) differs, [2] undecided lanes, [3] pairs outside the guards.
+__global__ void box_random(uint32_t seed, uint32_t n, int mode, unsigned long long *cnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t h = mix32(seed ^ mix32(i * 16u + 1u));
+    auto next = [&]() { return h = mix32(h + 0x9E3779B9u); };
+    float o[3], d[3], p[3];
+    const float t = 0.5f + float(next() >> 8) * (16.0f / 16777216.0f);
+    for (int k = 0; k < 3; ++k) {
+        o[k] = float(int32_t(next() >> 16) - 32768) * (4.0f / 32768.0f);
+        d[k] = guard_dir(next(), next());
+        d[k] = fminf(fmaxf(d[k], -64.0f), 64.0f);
+        if (fabsf(d[k]) < 0x1p-20f) d[k] = 1.0f;
+        p[k] = o[k] + d[k] * t;
+    }
+    PtAabb b{};
+    for (int k = 0; k < 3; ++k) {
+        const float r1 = 0.01f + float(next() >> 8) * (2.0f / 16777216.0f);
+        const float r2 = 0.01f + float(next() >> 8) * (2.0f / 16777216.0f);
+        b.bmin[k] = p[k] - r1;
+        b.bmax[k] = p[k] + r2;
+    }
+    if (mode == 1) {  // entry through face a1 and exit through face a2 at p, jittered by a few ulps
+        const int a1 = int(next() % 3u), a2 = (a1 + 1 + int(next() % 2u)) % 3;
+        const int u1 = int(next() % 9u) - 4, u2 = int(next() % 9u) - 4;
+        if (d[a1] > 0.0f) b.bmin[a1] = __uint_as_float(__float_as_uint(p[a1]) + uint32_t(u1));
+        else b.bmax[a1] = __uint_as_float(__float_as_uint(p[a1]) + uint32_t(u1));
+        if (d[a2] > 0.0f) b.bmax[a2] = __uint_as_float(__float_as_uint(p[a2]) + uint32_t(u2));
+        else b.bmin[a2] = __uint_as_float(__float_as_uint(p[a2]) + uint32_t(u2));
+    }
+    bool ok = true;
+    for (int k = 0; k < 3; ++k)
+        ok = ok && pt_div_coord_ok(o[k]) && pt_div_dir_ok(d[k]) && pt_div_coord_ok(b.bmin[k]) &&
+             pt_div_coord_ok(b.bmax[k]);
+    if (!ok) {
+        atomicAdd(cnt + 3, 1ull);
+        return;
+    }
+    const float yx = 1.0f / d[0], yy = 1.0f / d[1], yz = 1.0f / d[2];
+    float gap = __builtin_inff();
+    const bool approx = pt::ray_box_approx(b, o[0], o[1], o[2], yx, yy, yz, gap);
+    const bool want = pt::ray_box(b, o[0], o[1], o[2], d[0], d[1], d[2]);
+    if (gap > 0.0f) {
+        if (approx != want) atomicAdd(cnt + 0, 1ull);
+    } else {
+        atomicAdd(cnt + 2, 1ull);
+        if (pt::ray_box_rcp(b, o[0], o[1], o[2], d[0], d[1], d[2], yx, yy, yz) != want) atomicAdd(cnt + 1, 1ull);
+    }
+}
+
 }  // namespace
+
+extern "C" int pt_check_box_random(int hip_device, uint32_t seed, uint32_t n, int mode, uint64_t *counts) {
+    if (!counts) return PT_ERR_INVALID;
+    if (hipSetDevice(hip_device) != hipSuccess) return PT_ERR_HIP;
+    unsigned long long *d = nullptr;
+    if (hipMalloc(&d, 4 * sizeof(*d)) != hipSuccess) return PT_ERR_HIP;
+    int rc = hipMemset(d, 0, 4 * sizeof(*d)) == hipSuccess ? PT_OK : PT_ERR_HIP;
+    if (rc == PT_OK && n > 0) {
+        hipLaunchKernelGGL(box_random, dim3((n + 255) / 256), dim3(256), 0, 0, seed, n, mode, d);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = PT_ERR_HIP;
+    }
+    unsigned long long h[4] = {0ull, 0ull, 0ull, 0ull};
+    if (rc == PT_OK && hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) rc = PT_ERR_HIP;
+    for (int k = 0; k < 4; ++k) counts[k] = h[k];
+    (void)hipFree(d);
+    return rc;
+}
 
 extern "C" int pt_check_div_exhaustive(int hip_device, uint32_t a0, uint32_t na, uint32_t b0, uint32_t nb,
                                        uint64_t *mismatches, uint64_t *first_bad) {

@@ -253,6 +253,12 @@ int pt_check_div_exhaustive(int hip_device, uint32_t a0, uint32_t na, uint32_t b
  * of two guarded coordinates, guarded divisor); a zero quotient may differ in
  * sign only. */
 int pt_check_div_random(int hip_device, uint32_t seed, uint32_t n, uint64_t *mismatches, uint64_t *first_bad);
+/* The margin-decided slab test of bounds() on n random
+ * guarded (box, ray) pairs; mode 1 puts the ray through a box edge (near
+ * ties).  counts[0]: decided pairs whose answer differs from the IEEE slab
+ * test, [1]: undecided pairs whose exact fallback differs, [2]: undecided
+ * pairs, [3]: pairs drawn outside the guards (skipped). */
+int pt_check_box_random(int hip_device, uint32_t seed, uint32_t n, int mode, uint64_t *counts);
 
 #ifdef __cplusplus
 }

@@ -90,3 +90,19 @@ def test_div_rcp_on_guarded_operands(gpu, seed):
     bad, first = ctypes.c_uint64(), ctypes.c_uint64()
     assert N.lib().pt_check_div_random(0, seed, 1 << 28, ctypes.byref(bad), ctypes.byref(first)) == N.PT_OK
     assert bad.value == 0, hex(first.value)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_margin_decided_slab_test(gpu, mode):
+    """bounds()' slab test from reciprocal products: every pair
+    the margin decides agrees with the IEEE slab test; the undecided ones (ray
+    through a box edge, mode 1) agree after the exact fallback."""
+    counts = (ctypes.c_uint64 * 4)()
+    n = 1 << 24
+    assert N.lib().pt_check_box_random(0, 7 + mode, n, mode, counts) == N.PT_OK
+    decided_bad, exact_bad, undecided, skipped = list(counts)
+    print(f"mode {mode}: undecided {undecided} of {n}, skipped {skipped}")
+    assert decided_bad == 0 and exact_bad == 0
+    assert skipped < n // 4
+    if mode == 1:
+        assert undecided > 0  # the near-ties reach the fallback
