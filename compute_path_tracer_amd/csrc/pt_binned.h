@@ -155,8 +155,10 @@ __device__ __forceinline__ void pixel_of(const PtLaunch &L, uint32_t pl, int &x,
     y = (g / L.tiles_x) * PT_TILE + (p >> 3);
 }
 
-// gen: camera ray + bounds() of every (frame, pixel) of the chunk.
-template <bool ST>
+// gen: camera ray + bounds() of every (frame, pixel) of the chunk
+// (MapBounds<Map>: the generic box loop, or the scene kernels' straight-line
+// slab tests).
+template <class Map, bool ST>
 __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
     hist_zero(lh);
@@ -176,7 +178,7 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
         pt_f3 ro, rd;
         camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), L.width, L.height, L.aspect, L.fov, rng, ro, rd);
         st.add(PT_ST_SAMPLES);
-        const uint4 m = bounds_mask<ST>(L, ro, rd, st);
+        const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
         store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, pt_f3{0.0f, 0.0f, 0.0f}, rng, i, m.x, m.y);
         if (P.wide) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t b = bin_of(m);

@@ -35,6 +35,8 @@ struct PtJitModule {
     hipFunction_t trace_m_stats = nullptr;
     hipFunction_t shade_t = nullptr;        // shade pass with the normal taps (JitMapB)
     hipFunction_t shade_t_stats = nullptr;
+    hipFunction_t gen = nullptr;  // camera rays + the scene's straight-line bounds()
+    hipFunction_t gen_stats = nullptr;
     std::string key;  // generated source
 };
 

@@ -829,9 +829,19 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
             for (int i = 1; i < nl; ++i) HIPCHK(c, hipStreamWaitEvent(c->lane[i].stream, c->fork_ev, 0));
         }
+        static const int gen_jit = [] {  // A/B knob: PT_GEN_JIT=0 keeps the ahead-of-time gen kernel
+            const char *v = std::getenv("PT_GEN_JIT");
+            return v ? std::atoi(v) : 1;
+        }();
         for (int i = 0; i < nl; ++i) {
-            pt_launch_bin(PtBinStage::Gen, P[i], stats, item_grid(size_t(P[i].n_src_const)), c->lane[i].stream);
-            HIPCHK(c, hipGetLastError());
+            if (jit && gen_jit) {
+                void *args[] = {&P[i]};
+                HIPCHK(c, hipModuleLaunchKernel(stats ? jm->gen_stats : jm->gen, item_grid(size_t(P[i].n_src_const)), 1,
+                                                1, PT_BIN_BLOCK, 1, 1, 0, c->lane[i].stream, args, nullptr));
+            } else {
+                pt_launch_bin(PtBinStage::Gen, P[i], stats, item_grid(size_t(P[i].n_src_const)), c->lane[i].stream);
+                HIPCHK(c, hipGetLastError());
+            }
         }
         // shade the hits trace pass k wrote into ray[(k + 1) & 1]: ended paths
         // store their colour, the rest get their next ray, bounds() and bin
