@@ -4,8 +4,8 @@
 Workload (BASELINE.json configs[2], the metric's "1920x1080x8-bounce"): the
 32-node sdf_editor graph (scenes.c3_graph32), 1920x1080, 8 bounces, progressive
 accumulation, 256 spp per render.  One *step* = one pt_dispatch of ``--spp``
-(default 16) frames per pixel over this rank's tiles; 16 steps = the 256-spp
-render.  Inputs (scene tables, image) are resident in HBM before timing.
+(default 256: the whole C3 render) frames per pixel over this rank's tiles.
+Inputs (scene tables, image) are resident in HBM before timing.
 
 Multi-GPU (``torchrun --nproc-per-node N``): cyclic 8x8-tile ownership, each
 rank renders its 1/N of the tiles for N*spp frames per step (weak scaling:
@@ -171,8 +171,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--spp", type=int, default=64,
-                    help="frames per pixel per step (per GPU-share); 4 steps x 64 = the 256-spp C3 config")
+    ap.add_argument("--spp", type=int, default=256,
+                    help="frames per pixel per step (per GPU-share); 256 = one step is the whole C3 render")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=8)

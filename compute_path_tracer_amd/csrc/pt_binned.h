@@ -553,9 +553,11 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                     store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, uint32_t(mat), 0u);
                     P.hitn[pos] = make_float4(dv0, dv1, dv2, 0.0f);
                 } else {  // hit point + check[] + tap bound + material (bin_shade_body)
+#ifndef PT_EXP_NOSTORE  // (timing experiment only: hit records not written, images wrong)
                     store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, uint32_t(ck.lo), uint32_t(ck.lo >> 32));
                     P.hitn[pos] = make_float4(dv0, __uint_as_float(uint32_t(mat)), __uint_as_float(uint32_t(ck.hi)),
                                               __uint_as_float(uint32_t(ck.hi >> 32)));
+#endif
                 }
                 P.key[pos] = PT_BIN_HIT;
             }

@@ -65,7 +65,7 @@ struct pt_ctx {
     int shade_batch = -1;  // -1 = environment / default
     int jit = -1;          // 1 use per-scene hipRTC kernels, 0 interpreter; -1 = env (PT_JIT), default 1
     int jit_bake = -1;     // 0 values from the node table, 1 baked as literals, 2 tier-up; -1 = env (PT_JIT_BAKE), default 2
-    int bin_samples = -1;  // binned pipeline: samples per chunk; -1 = env (PT_BIN_SAMPLES), default 2^27
+    int bin_samples = -1;  // binned pipeline: samples per chunk; -1 = env (PT_BIN_SAMPLES), default 2^29
     PtJitModule jit_mod;   // scene kernel for the topology (key = its source)
     // tier-up (jit_bake 2): the same kernel with the current values baked in as
     // literals, compiled on a worker thread and used once ready while the
@@ -626,7 +626,17 @@ static size_t bin_samples(const pt_ctx *c) {
         const char *v = std::getenv("PT_BIN_SAMPLES");
         return v ? std::atol(v) : 0L;
     }();
-    return env >= 64 ? size_t(env) : (size_t(1) << 27);  // 23.6 GB of HBM; larger chunks shorten per-pass tails
+    if (env >= 64) return size_t(env);
+    // default: 2^29 samples (a whole 256-spp 1080p render: 94 GB of HBM at
+    // 176 B per sample; every pass's tail is paid once per chunk, so larger
+    // chunks are faster: 64 -> 256 frames per chunk +5 %), at most half of
+    // the device's memory
+    static const size_t cap = [] {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || total_b == 0) return size_t(1) << 27;
+        return std::max<size_t>(size_t(1) << 20, total_b / 2 / 176);
+    }();
+    return std::min<size_t>(size_t(1) << 29, cap);
 }
 
 // Pipelines per chunk (1..kMaxLanes): pt_set_option "bin_lanes", else env PT_BIN_LANES.
@@ -675,7 +685,9 @@ static void free_bin(pt_ctx *c) {
 // Buffers for `lanes` pipelines of `samples` samples each.
 static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
     const size_t words = 4 * (passes + 1);
-    if (samples <= c->bin_cap && words <= c->ctrl_words && lanes <= c->n_lanes) return PT_OK;
+    // (mask_hi, check[] bits 64..127, exists only for scenes with > 64 entries)
+    const bool hi_ok = c->n_check <= 64 || (c->n_lanes > 0 && c->lane[0].mask_hi != nullptr);
+    if (samples <= c->bin_cap && words <= c->ctrl_words && lanes <= c->n_lanes && hi_ok) return PT_OK;
     HIPCHK(c, hipStreamSynchronize(c->stream));  // lane 1 joins lane 0's stream before every dispatch ends
     samples = std::max(samples, c->bin_cap);
     lanes = std::max(lanes, c->n_lanes);
@@ -685,7 +697,7 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
         pt_ctx::BinLane &l = c->lane[i];
         ok = hipMalloc(&l.ray[0], samples * sizeof(PtRay)) == hipSuccess &&
              hipMalloc(&l.ray[1], samples * sizeof(PtRay)) == hipSuccess &&
-             hipMalloc(&l.mask_hi, samples * sizeof(uint2)) == hipSuccess &&
+             (c->n_check <= 64 || hipMalloc(&l.mask_hi, samples * sizeof(uint2)) == hipSuccess) &&
              hipMalloc(&l.key, samples * sizeof(uint32_t)) == hipSuccess &&
              hipMalloc(&l.idx, samples * sizeof(uint32_t)) == hipSuccess &&
              hipMalloc(&l.hitn, samples * sizeof(float4)) == hipSuccess &&
