@@ -34,7 +34,9 @@
 #define PT_BIN_NONE 0xffffffffu
 #define PT_BIN_HIT 0xfffffffeu  // trace -> shade: a hit record was written at this position
 #define PT_BIN_BLOCK 256  // threads per block of the gen / bounds / scatter kernels
+#ifndef PT_SCATTER_ITEMS
 #define PT_SCATTER_ITEMS 16
+#endif
 
 struct PtRay {  // a path between two segments, 64 B
     float ro[3];

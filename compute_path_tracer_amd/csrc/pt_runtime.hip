@@ -777,6 +777,10 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         return v ? std::atoi(v) : 0;
     }();
     if (trace_cu_env > 0 && trace_cu_env < per_cu) per_cu = trace_cu_env;
+    // default: leave one wave slot per SIMD (4 per CU) to the other pipeline,
+    // so its shade / scatter / scan blocks run beside the persistent trace
+    // waves instead of waiting for a pass to drain (24 of 28: +1.5 %)
+    else if (trace_cu_env == 0 && per_cu > 8) per_cu -= 4;
     const unsigned trace_grid = cu * unsigned(std::max(1, per_cu));
     static const int run_max = [] {  // A/B knob
         const char *v = std::getenv("PT_BIN_RUN");
