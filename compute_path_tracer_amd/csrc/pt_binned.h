@@ -29,7 +29,9 @@
 
 #include "pt_path.h"
 
+#ifndef PT_BIN_BITS
 #define PT_BIN_BITS 12
+#endif
 #define PT_BINS (1 << PT_BIN_BITS)
 #define PT_BIN_NONE 0xffffffffu
 #define PT_BIN_HIT 0xfffffffeu  // trace -> shade: a hit record was written at this position
