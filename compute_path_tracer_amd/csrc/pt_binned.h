@@ -71,6 +71,8 @@ struct PtPass {
     int32_t wide;           // check[] has more than 64 entries
     int32_t run_max;        // trace: longest run of binned rays a wave takes at once (multiple of 64)
     int32_t refill_min;     // trace: refill when at least this many lanes are free (or none map)
+    int32_t gen_order;      // gen: list the slots in generation order (idx; the host sets ctrl[0]) for the
+                            // first trace pass instead of binning them (a 64-ray window = one 8x8 tile)
 };
 
 namespace pt {
@@ -174,8 +176,12 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
         const uint32_t f = i / npix, pl = i - f * npix;
         int x, y;
         pixel_of(L, pl, x, y);
-        if (x >= L.width || y >= L.height) {
-            P.key[i] = PT_BIN_NONE;
+        const bool live = x < L.width && y < L.height;
+        // the first pass's list in generation order (the host takes this path
+        // only when every tile is full, so every slot is live)
+        if (P.gen_order) P.idx[i] = i;
+        if (!live) {
+            if (!P.gen_order) P.key[i] = PT_BIN_NONE;
             continue;
         }
         uint32_t rng;
@@ -185,11 +191,13 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
         store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, pt_f3{0.0f, 0.0f, 0.0f}, rng, i, m.x, m.y);
         if (P.wide) P.mask_hi[i] = make_uint2(m.z, m.w);
-        const uint32_t b = bin_of(m);
-        P.key[i] = b;
-        atomicAdd(&lh[b], 1u);
+        if (!P.gen_order) {
+            const uint32_t b = bin_of(m);
+            P.key[i] = b;
+            atomicAdd(&lh[b], 1u);
+        }
     }
-    hist_flush(lh, P.hist);
+    if (!P.gen_order) hist_flush(lh, P.hist);
     flush_stats<ST>(L, st);
 }
 

@@ -845,6 +845,21 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
             for (int i = 1; i < nl; ++i) HIPCHK(c, hipStreamWaitEvent(c->lane[i].stream, c->fork_ev, 0));
         }
+        // the first pass takes the primary rays in generation order (gen lists
+        // them, the host sets the count; no histogram, scan or scatter: +1 %);
+        // PT_GEN_BIN=1 bins them like every other pass
+        static const int gen_bin = [] {
+            const char *v = std::getenv("PT_GEN_BIN");
+            return v ? std::atoi(v) : 0;
+        }();
+        // (only when every local tile lies inside the image: then every
+        // generated slot is live and the list is the identity order)
+        const bool full_tiles = L.width % PT_TILE == 0 && L.height % PT_TILE == 0 && L.debug == 0;
+        for (int i = 0; i < nl && !gen_bin && full_tiles; ++i) {
+            P[i].gen_order = 1;
+            const uint32_t ctrl0[2] = {P[i].n_src_const, 0u};
+            HIPCHK(c, hipMemcpyAsync(c->lane[i].ctrl, ctrl0, sizeof ctrl0, hipMemcpyHostToDevice, c->lane[i].stream));
+        }
         static const int gen_jit = [] {  // A/B knob: PT_GEN_JIT=0 keeps the ahead-of-time gen kernel
             const char *v = std::getenv("PT_GEN_JIT");
             return v ? std::atoi(v) : 1;
@@ -887,9 +902,12 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 p.rout = l.ray[(k + 1) & 1];
                 p.ctrl = l.ctrl + 4 * k;
                 p.n_src = k == 0 ? nullptr : l.ctrl + 4 * (k - 1);
-                pt_launch_bin(PtBinStage::Scan, p, stats, 1, l.stream);
-                pt_launch_bin(PtBinStage::Scatter, p, stats, scatter_grid(k == 0 ? p.n_src_const : c->bin_cap), l.stream);
-                HIPCHK(c, hipGetLastError());
+                if (k > 0 || !p.gen_order) {
+                    pt_launch_bin(PtBinStage::Scan, p, stats, 1, l.stream);
+                    pt_launch_bin(PtBinStage::Scatter, p, stats, scatter_grid(k == 0 ? p.n_src_const : c->bin_cap),
+                                  l.stream);
+                    HIPCHK(c, hipGetLastError());
+                }
                 if (!stats) HIPCHK(c, record_trace_event(c, l.stream));
                 if (jit) {
                     void *args[] = {&p};
