@@ -77,22 +77,25 @@ def pipeline_bytes(st: dict, pixels: float) -> dict:
     (pt_binned.h), from the instrumented run's counters: S samples, G
     segments (rays entering a trace pass), H shaded hits.  Misses G - H end
     in the trace pass; G - S rays continue from a shade pass; H - (G - S)
-    paths end there.  Per pass and ray: gen writes the 64 B ray + 4 B key;
-    scatter reads every slot's 4 B key and writes a 4 B binned slot; trace
-    reads a slot (4 B) and its ray (64 B) and writes a colour + end marker
-    (16 + 4 B, miss) or a hit record + tap record + marker (64 + 16 + 4 B);
-    shade reads each slot's marker (4 B) and each hit's 64 + 16 B and writes
-    the next ray + key (64 + 4 B) or the colour + marker (16 + 4 B); fold
-    reads each frame's colour (16 B) and reads + writes the texel (32 B per
-    pixel).  Scenes with > 64 check[] entries add 8 B per ray move (not
-    counted here: the bench scene has 24)."""
+    paths end there.  Records are 64 B (PtRay).  gen writes each sample's
+    ray and zeroes its colour slot (64 + 16 B; the first pass takes the rays
+    in generation order, so its scan / scatter move nothing); scatter reads
+    every later slot's 4 B key and writes a 4 B binned slot; trace reads a
+    slot (4 B) and its ray (64 B) and writes a hit record + marker (64 + 4 B)
+    or a miss marker (4 B); shade reads each position's marker (4 B) and
+    each hit's record (64 B) and writes the next ray + key (64 + 4 B) or an
+    end marker (4 B); fold reads each frame's colour (16 B) and reads +
+    writes the texel (32 B per pixel).  Not counted: the colour slot's
+    read-modify-write at emitting hits (32 B each; no counter separates
+    them) and the 8 B high mask words of scenes with > 64 check[] entries
+    (the bench scene has 24)."""
     S, G, H = float(st["samples"]), float(st["segments"]), float(st["shaded"])
     cont, miss = G - S, G - H
     ended = H - cont
-    parts = {"gen": 68.0 * S,
-             "scatter": 8.0 * G,
-             "trace": 68.0 * G + 20.0 * miss + 84.0 * H,
-             "shade": 4.0 * G + 80.0 * H + 68.0 * cont + 20.0 * ended,
+    parts = {"gen": 80.0 * S,
+             "scatter": 8.0 * cont,
+             "trace": 68.0 * G + 68.0 * H + 4.0 * miss,
+             "shade": 68.0 * H + 68.0 * cont + 4.0 * ended,
              "fold": 16.0 * S + 32.0 * pixels}
     parts["total"] = sum(parts.values())
     return parts

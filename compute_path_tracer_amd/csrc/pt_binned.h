@@ -40,15 +40,21 @@
 #define PT_SCATTER_ITEMS 16
 #endif
 
-struct PtRay {  // a path between two segments, 64 B
-    float ro[3];
-    float rd[3];
-    float thr[3];
-    float ret[3];
-    uint32_t rng;
-    uint32_t sid;      // sample slot: frame * n_pix + local pixel
-    uint32_t mask[2];  // ray: check[] bits 0..63 of the segment (64..127: PtPass.mask_hi)
-                       // hit: [0] material index (normal differences in PtPass.hitn)
+// A path between two segments (ray) or at the hit of its segment (hit
+// record), 64 B = four 16 B quads:
+//   q0 = (ro.x, ro.y, ro.z, rd.x)        ro: origin, or the hit point
+//   q1 = (rd.y, rd.z, thr.x, thr.y)
+//   q2 = (thr.z, rng, sid, aux)          sid: sample slot = frame * n_pix + local
+//                                        pixel; aux: the hit's material index
+//   q3 = ray: check[] bits 0..63 of the segment to trace (64..127: PtPass.mask_hi)
+//        hit, taps in the shade pass: (check[] bits 0..63, the taps' map()
+//        bound, 0) (bits 64..127 in PtPass.hitn.zw)
+//        hit, taps in the trace pass: (calc_normal's differences, 0)
+// The path's radiance (path_trace's `ret`) is not carried: it lives in the
+// sample's colour slot (zeroed by gen), which the shade pass updates when an
+// emission is added and which is final when the path ends.
+struct PtRay {
+    uint4 q[4];
 };
 
 struct PtPass {
@@ -63,7 +69,7 @@ struct PtPass {
     uint32_t *ctrl;         // this pass: [0] binned rays, [1] trace run cursor
     const uint32_t *n_src;  // rin slots (bounds / scatter), null: n_src_const
     float4 *color;          // [frames][n_pix] sample colours
-    float4 *hitn;           // trace -> shade: calc_normal's differences per rout position
+    float4 *hitn;           // trace -> shade: check[] bits 64..127 of a hit (.zw; scenes with > 64 entries)
     uint32_t n_src_const;
     int32_t bounce;         // segment index of this pass (path_trace's loop counter i)
     int32_t n_pix;          // local pixel slots: n_tiles * 64
@@ -134,13 +140,12 @@ struct MapBounds {
     }
 };
 
-__device__ __forceinline__ void store_ray(PtRay *r, const pt_f3 &ro, const pt_f3 &rd, const pt_f3 &thr,
-                                          const pt_f3 &ret, uint32_t rng, uint32_t sid, uint32_t m0, uint32_t m1) {
-    float4 *v = reinterpret_cast<float4 *>(r);
-    v[0] = make_float4(ro.x, ro.y, ro.z, rd.x);
-    v[1] = make_float4(rd.y, rd.z, thr.x, thr.y);
-    v[2] = make_float4(thr.z, ret.x, ret.y, ret.z);
-    reinterpret_cast<uint4 *>(r)[3] = make_uint4(rng, sid, m0, m1);
+__device__ __forceinline__ void store_ray(PtRay *r, const pt_f3 &ro, const pt_f3 &rd, const pt_f3 &thr, uint32_t rng,
+                                          uint32_t sid, uint32_t aux, const uint4 &q3) {
+    r->q[0] = make_uint4(__float_as_uint(ro.x), __float_as_uint(ro.y), __float_as_uint(ro.z), __float_as_uint(rd.x));
+    r->q[1] = make_uint4(__float_as_uint(rd.y), __float_as_uint(rd.z), __float_as_uint(thr.x), __float_as_uint(thr.y));
+    r->q[2] = make_uint4(__float_as_uint(thr.z), rng, sid, aux);
+    r->q[3] = q3;
 }
 
 __device__ __forceinline__ void hist_zero(uint32_t *lh) {
@@ -189,7 +194,8 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
         camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), L.width, L.height, L.aspect, L.fov, rng, ro, rd);
         st.add(PT_ST_SAMPLES);
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
-        store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, pt_f3{0.0f, 0.0f, 0.0f}, rng, i, m.x, m.y);
+        store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, rng, i, 0u, make_uint4(m.x, m.y, 0u, 0u));
+        P.color[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the path's radiance (ret) starts at 0
         if (P.wide) P.mask_hi[i] = make_uint2(m.z, m.w);
         if (!P.gen_order) {
             const uint32_t b = bin_of(m);
@@ -225,26 +231,29 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     stt.init();
     const PtLaunch &L = P.L;
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
-    auto shade_one = [&](uint32_t i, const float4 &a, const float4 &b, const float4 &c, const uint4 &d,
-                         const float4 &nd) {
-        pt_f3 ro{a.x, a.y, a.z}, rd{a.w, b.x, b.y}, thr{b.z, b.w, c.x}, ret{c.y, c.z, c.w};
-        uint32_t rng = d.x;
+    auto shade_one = [&](uint32_t i, const uint4 &q0, const uint4 &q1, const uint4 &q2, const uint4 &q3,
+                         const uint2 &hi) {
+        pt_f3 ro{__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
+        pt_f3 rd{__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
+        pt_f3 thr{__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
+        pt_f3 ret{0.0f, 0.0f, 0.0f};  // this segment's emission (added to the colour slot below)
+        uint32_t rng = q2.y;
+        const uint32_t sid = q2.z;
+        const int mat = int(q2.w);
         int seg = P.bounce;
-        float dv0 = nd.x, dv1 = nd.y, dv2 = nd.z;
-        int mat = int(d.z);
+        // taps in the trace pass: q3 = calc_normal's differences
+        float dv0 = __uint_as_float(q3.x), dv1 = __uint_as_float(q3.y), dv2 = __uint_as_float(q3.z);
         if constexpr (!TAPS) {
             // (the taps' counters go to their own half of the stats buffer:
             // pt_dispatch_stats sums both, bench.py splits the flops by pass)
-            // hit record: d.z/d.w = check[] bits 0..63, nd = {tap bound, material, check[] bits 64..127}
-            const Check ck{uint64_t(d.z) | (uint64_t(d.w) << 32),
-                           uint64_t(__float_as_uint(nd.z)) | (uint64_t(__float_as_uint(nd.w)) << 32)};
-            const float bnd = nd.x;
+            // hit record: q3 = {check[] bits 0..63, tap bound}, hi = check[] bits 64..127
+            const Check ck{uint64_t(q3.x) | (uint64_t(q3.y) << 32), uint64_t(hi.x) | (uint64_t(hi.y) << 32)};
+            const float bnd = __uint_as_float(q3.z);
             // bnd widened by the taps' spread (two taps are at most 2e apart,
             // plus their coordinates' rounding): the first tap's tests against
             // it leave in `live` every shape any tap may need
             const float bndw = bnd + (0x1.a3ap-13f + 0x1p-20f * (fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z)));
             uint64_t live = 0ull;
-            mat = int(__float_as_uint(nd.y));
             float dp = 0.0f;
 #pragma unroll 1
             for (int k = 0; k < 6; ++k) {
@@ -266,14 +275,27 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             stt.add(PT_ST_NORMAL_MAPS, 6);
         }
         const bool done = shade_lane<ST>(L.mats, L.bounces, mat, dv0, dv1, dv2, 0, rng, ro, rd, thr, ret, seg, st);
+        // ret += emission * throughput (test_compute.glsl:148) on the colour
+        // slot: 0 + e, added to the slot, equals the slot plus e (a slot
+        // never holds -0), and a zero e changes no slot, so only emitting
+        // segments touch it
+        if (ret.x != 0.0f || ret.y != 0.0f || ret.z != 0.0f) {
+            float4 c = P.color[sid];
+            c.x += ret.x;
+            c.y += ret.y;
+            c.z += ret.z;
+            P.color[sid] = c;
+        }
         if (done) {
-            const pt_f3 col = final_color(L.debug, seg, L.bounces, ret);
-            P.color[d.y] = make_float4(col.x, col.y, col.z, 0.0f);
+            if (L.debug == 3) {  // bounce-count view: the colour is the segment count, not the radiance
+                const pt_f3 col = final_color(L.debug, seg, L.bounces, ret);
+                P.color[sid] = make_float4(col.x, col.y, col.z, 0.0f);
+            }
             P.key[i] = PT_BIN_NONE;
             return;
         }
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
-        store_ray(P.rin + i, ro, rd, thr, ret, rng, d.y, m.x, m.y);
+        store_ray(P.rin + i, ro, rd, thr, rng, sid, 0u, make_uint4(m.x, m.y, 0u, 0u));
         if (P.wide) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);
         P.key[i] = k;
@@ -283,12 +305,14 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     // each thread takes one position and loads its record together with the
     // marker: one memory round trip instead of two.
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const float4 *v = reinterpret_cast<const float4 *>(P.rin + i);
         const uint32_t key = P.key[i];
-        const float4 a = v[0], b = v[1], c = v[2];
-        const uint4 d = reinterpret_cast<const uint4 *>(P.rin + i)[3];
-        const float4 nd = P.hitn[i];
-        if (key == PT_BIN_HIT) shade_one(i, a, b, c, d, nd);
+        const uint4 q0 = P.rin[i].q[0], q1 = P.rin[i].q[1], q2 = P.rin[i].q[2], q3 = P.rin[i].q[3];
+        uint2 hi = make_uint2(0u, 0u);
+        if (!TAPS && P.wide) {
+            const float4 nd = P.hitn[i];
+            hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
+        }
+        if (key == PT_BIN_HIT) shade_one(i, q0, q1, q2, q3, hi);
     }
     hist_flush(lh, P.hist);
     flush_stats<ST>(L, st);
@@ -449,7 +473,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     int state = ST_FREE;
     uint32_t rng = 0u, sid = 0u, pos = 0u;
     pt_f3 ro{0.0f, 0.0f, 0.0f}, rd{0.0f, 0.0f, 1.0f};
-    pt_f3 thr{1.0f, 1.0f, 1.0f}, ret{0.0f, 0.0f, 0.0f};
+    pt_f3 thr{1.0f, 1.0f, 1.0f};
     int step = 0, mat = 0;  // (a lane's segment index is this pass's P.bounce)
     float t = 0.0f;
     float dv0 = 0.0f, dv1 = 0.0f, dv2 = 0.0f;
@@ -473,7 +497,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 const bool mapping_now = state == ST_MARCH || (TAPS && state == ST_NORMAL);
                 const bool in_win = uint32_t(lane) < wcnt;
                 ck.alo = wave_or_u64((mapping_now ? ck.lo : 0ull) |
-                                     (in_win ? (uint64_t(s3.z) | (uint64_t(s3.w) << 32)) : 0ull));
+                                     (in_win ? (uint64_t(s3.x) | (uint64_t(s3.y) << 32)) : 0ull));
                 ck.ahi = P.wide ? wave_or_u64((mapping_now ? ck.hi : 0ull) |
                                               (in_win ? (uint64_t(sh.x) | (uint64_t(sh.y) << 32)) : 0ull))
                                 : 0ull;
@@ -512,10 +536,12 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 ro = pt_f3{a0, a1, a2};
                 rd = pt_f3{a3, b0, b1};
                 thr = pt_f3{b2, b3, c0};
-                ret = pt_f3{c1, c2, c3};
-                rng = d0;
-                sid = d1;
-                ck.lo = uint64_t(d2) | (uint64_t(d3) << 32);
+                rng = __float_as_uint(c1);
+                sid = __float_as_uint(c2);
+                (void)c3;
+                ck.lo = uint64_t(d0) | (uint64_t(d1) << 32);
+                (void)d2;
+                (void)d3;
                 ck.hi = uint64_t(e0) | (uint64_t(e1) << 32);
                 pos = wbase + uint32_t(src);
                 t = 0.0f;
@@ -553,23 +579,26 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         }
         tm = st.lap(PT_ST_CYC_MAP, tm);
 
-        // ---- 3. hand finished segments on: a miss ends the path (its colour
-        // is final), a hit goes to the shade pass with its normal differences
+        // ---- 3. hand finished segments on: a miss ends the path (its
+        // colour slot already holds its radiance), a hit goes to the shade
+        // pass as one 64 B record (PtRay)
         if (state == ST_SHADE) {
             if (step < 0) {
-                const pt_f3 c = final_color(L.debug, P.bounce, L.bounces, ret);
-                P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
+                if (L.debug == 3) {  // bounce-count view
+                    const pt_f3 c = final_color(L.debug, P.bounce, L.bounces, pt_f3{0.0f, 0.0f, 0.0f});
+                    P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
+                }
                 P.key[pos] = PT_BIN_NONE;
             } else {
-                if constexpr (TAPS) {
-                    store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, uint32_t(mat), 0u);
-                    P.hitn[pos] = make_float4(dv0, dv1, dv2, 0.0f);
+                if constexpr (TAPS) {  // normal differences
+                    store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
+                              make_uint4(__float_as_uint(dv0), __float_as_uint(dv1), __float_as_uint(dv2), 0u));
                 } else {  // hit point + check[] + tap bound + material (bin_shade_body)
-#ifndef PT_EXP_NOSTORE  // (timing experiment only: hit records not written, images wrong)
-                    store_ray(P.rout + pos, ro, rd, thr, ret, rng, sid, uint32_t(ck.lo), uint32_t(ck.lo >> 32));
-                    P.hitn[pos] = make_float4(dv0, __uint_as_float(uint32_t(mat)), __uint_as_float(uint32_t(ck.hi)),
-                                              __uint_as_float(uint32_t(ck.hi >> 32)));
-#endif
+                    store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
+                              make_uint4(uint32_t(ck.lo), uint32_t(ck.lo >> 32), __float_as_uint(dv0), 0u));
+                    if (P.wide)
+                        P.hitn[pos] = make_float4(0.0f, 0.0f, __uint_as_float(uint32_t(ck.hi)),
+                                                  __uint_as_float(uint32_t(ck.hi >> 32)));
                 }
                 P.key[pos] = PT_BIN_HIT;
             }

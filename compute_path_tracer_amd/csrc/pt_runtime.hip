@@ -616,9 +616,9 @@ int pt_set_tiles(pt_ctx *c, uint32_t rank, uint32_t nranks) {
 }
 
 // ---- binned pipeline (pt_binned.h) -------------------------------------------
-// per sample of a chunk: two ray buffers, high mask words, bin key, binned slot, colour, hit normal
-constexpr size_t kBinBytesPerSample =
-    2 * sizeof(PtRay) + sizeof(uint2) + 2 * sizeof(uint32_t) + sizeof(float4) + sizeof(float4);
+// per sample of a chunk: two ray buffers, bin key, binned slot, colour (+ the
+// high mask words and hit records' high check[] words of scenes with > 64 entries)
+constexpr size_t kBinBytesPerSample = 2 * sizeof(PtRay) + 2 * sizeof(uint32_t) + sizeof(float4);
 
 static size_t bin_samples(const pt_ctx *c) {
     if (c->bin_samples > 0) return size_t(c->bin_samples);
@@ -627,14 +627,14 @@ static size_t bin_samples(const pt_ctx *c) {
         return v ? std::atol(v) : 0L;
     }();
     if (env >= 64) return size_t(env);
-    // default: 2^29 samples (a whole 256-spp 1080p render: 94 GB of HBM at
-    // 176 B per sample; every pass's tail is paid once per chunk, so larger
+    // default: 2^29 samples (a whole 256-spp 1080p render: 82 GB of HBM at
+    // 152 B per sample; every pass's tail is paid once per chunk, so larger
     // chunks are faster: 64 -> 256 frames per chunk +5 %), at most half of
     // the device's memory
     static const size_t cap = [] {
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || total_b == 0) return size_t(1) << 27;
-        return std::max<size_t>(size_t(1) << 20, total_b / 2 / 176);
+        return std::max<size_t>(size_t(1) << 20, total_b / 2 / kBinBytesPerSample);
     }();
     return std::min<size_t>(size_t(1) << 29, cap);
 }
@@ -700,7 +700,7 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
              (c->n_check <= 64 || hipMalloc(&l.mask_hi, samples * sizeof(uint2)) == hipSuccess) &&
              hipMalloc(&l.key, samples * sizeof(uint32_t)) == hipSuccess &&
              hipMalloc(&l.idx, samples * sizeof(uint32_t)) == hipSuccess &&
-             hipMalloc(&l.hitn, samples * sizeof(float4)) == hipSuccess &&
+             (c->n_check <= 64 || hipMalloc(&l.hitn, samples * sizeof(float4)) == hipSuccess) &&
              hipMalloc(&l.hist, PT_BINS * sizeof(uint32_t)) == hipSuccess &&
              hipMalloc(&l.offs, PT_BINS * sizeof(uint32_t)) == hipSuccess &&
              hipMalloc(&l.ctrl, words * sizeof(uint32_t)) == hipSuccess;
