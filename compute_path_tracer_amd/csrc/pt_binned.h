@@ -34,7 +34,7 @@
 #endif
 #define PT_BINS (1 << PT_BIN_BITS)
 #define PT_BIN_NONE 0xffffffffu
-#define PT_BIN_HIT 0xfffffffeu  // trace -> shade: a hit record was written at this position
+#define PT_AUX_MISS 0xffffffffu  // trace -> shade: PtRay q2.w of a position whose segment missed
 #define PT_BIN_BLOCK 256  // threads per block of the gen / bounds / scatter kernels
 #ifndef PT_SCATTER_ITEMS
 #define PT_SCATTER_ITEMS 16
@@ -45,7 +45,8 @@
 //   q0 = (ro.x, ro.y, ro.z, rd.x)        ro: origin, or the hit point
 //   q1 = (rd.y, rd.z, thr.x, thr.y)
 //   q2 = (thr.z, rng, sid, aux)          sid: sample slot = frame * n_pix + local
-//                                        pixel; aux: the hit's material index
+//                                        pixel; aux: the hit's material index, or
+//                                        PT_AUX_MISS (a miss writes only this quad)
 //   q3 = ray: check[] bits 0..63 of the segment to trace (64..127: PtPass.mask_hi)
 //        hit, taps in the shade pass: (check[] bits 0..63, the taps' map()
 //        bound, 0) (bits 64..127 in PtPass.hitn.zw)
@@ -62,7 +63,7 @@ struct PtPass {
     PtRay *rin;             // this pass's rays, by slot (gen / bounds: the rays being binned)
     PtRay *rout;            // trace: next pass's rays, by binned position
     uint2 *mask_hi;         // check[] bits 64..127 per rin slot (scenes with > 64 entries)
-    uint32_t *key;          // bin per rin slot (PT_BIN_NONE: no live ray); trace marks its rout positions NONE / HIT
+    uint32_t *key;          // bin per rin slot (PT_BIN_NONE: no live ray)
     uint32_t *idx;          // rin slots in bin order
     uint32_t *hist;         // [PT_BINS] counts, zero outside gen/bounds -> scan
     uint32_t *offs;         // [PT_BINS] scatter cursors
@@ -302,17 +303,17 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         atomicAdd(&lh[k], 1u);
     };
     // Nearly every position holds a hit (misses end in the trace pass), so
-    // each thread takes one position and loads its record together with the
-    // marker: one memory round trip instead of two.
+    // each thread takes one position and loads its whole record (a miss
+    // marks its record's q2): one memory round trip.
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t key = P.key[i];
         const uint4 q0 = P.rin[i].q[0], q1 = P.rin[i].q[1], q2 = P.rin[i].q[2], q3 = P.rin[i].q[3];
         uint2 hi = make_uint2(0u, 0u);
         if (!TAPS && P.wide) {
             const float4 nd = P.hitn[i];
             hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
         }
-        if (key == PT_BIN_HIT) shade_one(i, q0, q1, q2, q3, hi);
+        if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
+        else shade_one(i, q0, q1, q2, q3, hi);
     }
     hist_flush(lh, P.hist);
     flush_stats<ST>(L, st);
@@ -588,7 +589,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                     const pt_f3 c = final_color(L.debug, P.bounce, L.bounces, pt_f3{0.0f, 0.0f, 0.0f});
                     P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
                 }
-                P.key[pos] = PT_BIN_NONE;
+                P.rout[pos].q[2] = make_uint4(0u, 0u, sid, PT_AUX_MISS);
             } else {
                 if constexpr (TAPS) {  // normal differences
                     store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
@@ -600,7 +601,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                         P.hitn[pos] = make_float4(0.0f, 0.0f, __uint_as_float(uint32_t(ck.hi)),
                                                   __uint_as_float(uint32_t(ck.hi >> 32)));
                 }
-                P.key[pos] = PT_BIN_HIT;
             }
             state = ST_FREE;
         }
