@@ -367,9 +367,36 @@ __device__ __forceinline__ void bin_scan_body(const PtPass &P) {
 
 // scatter: ray slots into bin order.  Per block tile, the slots of one bin
 // take consecutive places (LDS ranks) after one global reservation.
+#ifndef PT_SCATTER_V
+#define PT_SCATTER_V 2
+#endif
 __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
     __shared__ uint32_t cnt[PT_BINS];
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
+#if PT_SCATTER_V == 2
+    // One contiguous run of the slots per block: count its bins in LDS,
+    // reserve each bin's places with one global atomic for the whole run
+    // (not one per 4096-slot tile), then read the keys again and hand out
+    // the places with LDS cursors.
+    const uint32_t per = ((n + gridDim.x - 1u) / gridDim.x + PT_BIN_BLOCK - 1u) & ~uint32_t(PT_BIN_BLOCK - 1);
+    const uint32_t b0 = min(n, blockIdx.x * per), b1 = min(n, b0 + per);
+    hist_zero(cnt);
+    for (uint32_t e = b0 + threadIdx.x; e < b1; e += PT_BIN_BLOCK) {
+        const uint32_t k = P.key[e];
+        if (k != PT_BIN_NONE) atomicAdd(&cnt[k], 1u);
+    }
+    __syncthreads();
+    for (int b = int(threadIdx.x); b < PT_BINS; b += PT_BIN_BLOCK) {
+        const uint32_t c = cnt[b];
+        if (c != 0u) cnt[b] = atomicAdd(&P.offs[b], c);
+    }
+    __syncthreads();
+    for (uint32_t e = b0 + threadIdx.x; e < b1; e += PT_BIN_BLOCK) {
+        const uint32_t k = P.key[e];
+        if (k != PT_BIN_NONE) P.idx[atomicAdd(&cnt[k], 1u)] = e;
+    }
+    return;
+#endif
     const uint32_t tile = PT_BIN_BLOCK * PT_SCATTER_ITEMS;
     for (uint32_t t0 = blockIdx.x * tile; t0 < n; t0 += gridDim.x * tile) {
         hist_zero(cnt);

@@ -760,7 +760,11 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     };
     auto scatter_grid = [&](size_t n) {
         const size_t tile = PT_BIN_BLOCK * PT_SCATTER_ITEMS;
-        return unsigned(std::max<size_t>(1, std::min<size_t>((n + tile - 1) / tile, 4 * cu)));
+        static const size_t per_cu = [] {
+            const char *e = std::getenv("PT_SCATTER_GRID");
+            return size_t(e && std::atoi(e) > 0 ? std::atoi(e) : 4);
+        }();
+        return unsigned(std::max<size_t>(1, std::min<size_t>((n + tile - 1) / tile, per_cu * cu)));
     };
     const PtJitModule *jm = jit_active(c);
     const bool jit = jm != nullptr;
