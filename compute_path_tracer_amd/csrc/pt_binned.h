@@ -80,6 +80,9 @@ struct PtPass {
     int32_t refill_min;     // trace: refill when at least this many lanes are free (or none map)
     int32_t gen_order;      // gen: list the slots in generation order (idx; the host sets ctrl[0]) for the
                             // first trace pass instead of binning them (a 64-ray window = one 8x8 tile)
+    int32_t gen_trace;      // first pass without a gen pass (scene kernels, generation order): the trace
+                            // pass makes each window's camera rays and bounds() itself, a miss zeroes its
+                            // colour slot, and the shade pass stores (not adds) the first segment's emission
 };
 
 namespace pt {
@@ -280,7 +283,9 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         // slot: 0 + e, added to the slot, equals the slot plus e (a slot
         // never holds -0), and a zero e changes no slot, so only emitting
         // segments touch it
-        if (ret.x != 0.0f || ret.y != 0.0f || ret.z != 0.0f) {
+        if (P.gen_trace) {  // first segment, no gen pass: the slot was never zeroed; 0 + e = e
+            P.color[sid] = make_float4(ret.x, ret.y, ret.z, 0.0f);
+        } else if (ret.x != 0.0f || ret.y != 0.0f || ret.z != 0.0f) {
             float4 c = P.color[sid];
             c.x += ret.x;
             c.y += ret.y;
@@ -430,7 +435,12 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
 //
 // TAPS = false: a lane stops at the hit (calc_point) and writes the hit
 // record for the shade pass, which evaluates the normal taps (bin_shade_body).
-template <class Map, bool ST, bool TAPS = true>
+//
+// GEN (PtPass gen_trace, the first pass in generation order): a window's
+// rays are not loaded but made here, lane j the camera ray and bounds() mask
+// of sample wbase + j -- what gen would have written (bin_gen_body), with
+// all 64 lanes at once -- so the chunk needs no gen pass.
+template <class Map, bool ST, bool TAPS = true, bool GEN = false>
 __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     // the staged window, once its loads have landed: [part][lane], so a
     // refill reads a ray with 4 ds_read_b128 instead of 16 cross-lane moves
@@ -470,7 +480,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     // next window: its slots, one per lane
     uint32_t nb = 0u, nc = 0u, nslot = 0u;
     next_window(nb, nc);
-    if (uint32_t(lane) < nc) nslot = P.idx[nb + uint32_t(lane)];
+    if (!GEN && uint32_t(lane) < nc) nslot = P.idx[nb + uint32_t(lane)];
     // staged window: lane j holds the ray of binned position wbase + j
     uint32_t wbase = 0u, wcnt = 0u, wtake = 0u;
     float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0, s2 = s0;
@@ -482,7 +492,22 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         wcnt = nc;
         wtake = 0u;
         in_lds = false;
-        if (uint32_t(lane) < wcnt) {
+        if (GEN && uint32_t(lane) < wcnt) {
+            const uint32_t i = wbase + uint32_t(lane), npix = uint32_t(P.n_pix);
+            const uint32_t f = i / npix, pl = i - f * npix;
+            int x, y;
+            pixel_of(L, pl, x, y);
+            uint32_t rg;
+            pt_f3 o, d;
+            camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), L.width, L.height, L.aspect, L.fov, rg, o, d);
+            st.add(PT_ST_SAMPLES);
+            const uint4 m = MapBounds<Map>::template mask<ST>(L, o, d, st);
+            s0 = make_float4(o.x, o.y, o.z, d.x);
+            s1 = make_float4(d.y, d.z, 1.0f, 1.0f);
+            s2 = make_float4(1.0f, __uint_as_float(rg), __uint_as_float(i), 0.0f);
+            s3 = make_uint4(m.x, m.y, 0u, 0u);
+            sh = make_uint2(m.z, m.w);
+        } else if (uint32_t(lane) < wcnt) {
             const uint4 *v = reinterpret_cast<const uint4 *>(P.rin + nslot);
             const uint4 a = v[0], b = v[1], c = v[2];
             s0 = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
@@ -493,7 +518,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         }
         if (wcnt != 0u) {
             next_window(nb, nc);
-            if (uint32_t(lane) < nc) nslot = P.idx[nb + uint32_t(lane)];
+            if (!GEN && uint32_t(lane) < nc) nslot = P.idx[nb + uint32_t(lane)];
         }
     };
     stage();
@@ -617,6 +642,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                     P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
                 }
                 P.rout[pos].q[2] = make_uint4(0u, 0u, sid, PT_AUX_MISS);
+                if constexpr (GEN) P.color[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // (no gen pass zeroed it)
             } else {
                 if constexpr (TAPS) {  // normal differences
                     store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),

@@ -37,6 +37,7 @@ struct PtJitModule {
     hipFunction_t shade_t_stats = nullptr;
     hipFunction_t gen = nullptr;  // camera rays + the scene's straight-line bounds()
     hipFunction_t gen_stats = nullptr;
+    hipFunction_t trace_g = nullptr;  // first pass with its own camera rays (PtPass gen_trace)
     std::string key;  // generated source
 };
 

@@ -868,8 +868,16 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             const char *v = std::getenv("PT_GEN_JIT");
             return v ? std::atoi(v) : 1;
         }();
+        // no gen pass: the first trace pass makes its windows' camera rays
+        // itself (scene kernels, generation order; PT_GEN_TRACE=0 keeps gen)
+        static const int gen_trace = [] {
+            const char *v = std::getenv("PT_GEN_TRACE");
+            return v ? std::atoi(v) : 1;
+        }();
         for (int i = 0; i < nl; ++i) {
-            if (jit && gen_jit) {
+            if (gen_trace && P[i].gen_order && jit && taps_shade && !stats && jm->trace_g) {
+                P[i].gen_trace = 1;
+            } else if (jit && gen_jit) {
                 void *args[] = {&P[i]};
                 HIPCHK(c, hipModuleLaunchKernel(stats ? jm->gen_stats : jm->gen, item_grid(size_t(P[i].n_src_const)), 1,
                                                 1, PT_BIN_BLOCK, 1, 1, 0, c->lane[i].stream, args, nullptr));
@@ -901,6 +909,8 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 const pt_ctx::BinLane &l = c->lane[i];
                 PtPass &p = P[i];
                 if (k > 0 && (rc = shade(i, k - 1)) != PT_OK) return rc;
+                const bool gt = k == 0 && p.gen_trace;
+                if (k > 0) p.gen_trace = 0;  // (shade pass 0 above still had it)
                 p.bounce = k;
                 p.rin = l.ray[k & 1];
                 p.rout = l.ray[(k + 1) & 1];
@@ -915,7 +925,8 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 if (!stats) HIPCHK(c, record_trace_event(c, l.stream));
                 if (jit) {
                     void *args[] = {&p};
-                    HIPCHK(c, hipModuleLaunchKernel(jf, trace_grid, 1, 1, 64, 1, 1, 0, l.stream, args, nullptr));
+                    HIPCHK(c, hipModuleLaunchKernel(gt ? jm->trace_g : jf, trace_grid, 1, 1, 64, 1, 1, 0, l.stream, args,
+                                                    nullptr));
                 } else {
                     pt_launch_bin(PtBinStage::Trace, p, stats, trace_grid, l.stream);
                     HIPCHK(c, hipGetLastError());
