@@ -72,31 +72,39 @@ def algorithmic_flops(st: dict) -> float:
     return float(f)
 
 
-def pipeline_bytes(st: dict, pixels: float) -> dict:
+def pipeline_bytes(st: dict, pixels: float, gen_trace: bool = False) -> dict:
     """Algorithmic HBM bytes of one dispatch of the binned pipeline
     (pt_binned.h), from the instrumented run's counters: S samples, G
     segments (rays entering a trace pass), H shaded hits.  Misses G - H end
     in the trace pass; G - S rays continue from a shade pass; H - (G - S)
-    paths end there.  Records are 64 B (PtRay).  gen writes each sample's
-    ray and zeroes its colour slot (64 + 16 B; the first pass takes the rays
-    in generation order, so its scan / scatter move nothing); scatter reads
-    every later slot's 4 B key and writes a 4 B binned slot; trace reads a
-    slot (4 B) and its ray (64 B) and writes a hit record + marker (64 + 4 B)
-    or a miss marker (4 B); shade reads each position's marker (4 B) and
-    each hit's record (64 B) and writes the next ray + key (64 + 4 B) or an
-    end marker (4 B); fold reads each frame's colour (16 B) and reads +
-    writes the texel (32 B per pixel).  Not counted: the colour slot's
-    read-modify-write at emitting hits (32 B each; no counter separates
-    them) and the 8 B high mask words of scenes with > 64 check[] entries
-    (the bench scene has 24)."""
+    paths end there.  Records are 64 B (PtRay).
+    - gen writes each sample's ray and zeroes its colour slot (64 + 16 B)
+      and lists it (4 B) -- or, gen_trace (the bench default), there is no
+      gen pass: the first trace pass makes its rays, and each sample's
+      colour slot is written once in pass 0 (16 B: by the trace pass at a
+      miss, by the shade pass at a hit);
+    - scatter reads every later slot's 4 B key and writes a 4 B binned slot
+      (the first pass takes generation order);
+    - trace reads a slot (4 B) and its ray (64 B) (not in the first pass
+      with gen_trace) and writes a hit record (64 B) or a miss marker (16 B);
+    - shade reads each hit's record (64 B) and each miss's marker (16 B) and
+      writes the next ray + key (64 + 4 B) or a NONE key (4 B);
+    - fold reads each frame's colour (16 B) and reads + writes the texel
+      (32 B per pixel).
+    Not counted: the colour slot's read-modify-write at emitting hits after
+    the first (32 B each; no counter separates them) and the high mask words
+    of scenes with > 64 check[] entries (the bench scene has 24)."""
     S, G, H = float(st["samples"]), float(st["segments"]), float(st["shaded"])
     cont, miss = G - S, G - H
     ended = H - cont
-    parts = {"gen": 80.0 * S,
+    traced_in = G - S if gen_trace else G
+    parts = {"gen": 0.0 if gen_trace else 84.0 * S,
              "scatter": 8.0 * cont,
-             "trace": 68.0 * G + 68.0 * H + 4.0 * miss,
-             "shade": 68.0 * H + 68.0 * cont + 4.0 * ended,
+             "trace": 68.0 * traced_in + 64.0 * H + 16.0 * miss,
+             "shade": 64.0 * H + 16.0 * miss + 68.0 * cont + 4.0 * (ended + miss),
              "fold": 16.0 * S + 32.0 * pixels}
+    if gen_trace:
+        parts["colour0"] = 16.0 * S
     parts["total"] = sum(parts.values())
     return parts
 
@@ -300,8 +308,8 @@ def main() -> None:
     flops_step = algorithmic_flops(st)
     rank_pixels = st["samples"] / max(1, spp_step)
     image_bytes = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per dispatch
-    pipe = pipeline_bytes(st, rank_pixels)
     jit = bool(pt.get_option("jit_active"))
+    pipe = pipeline_bytes(st, rank_pixels, gen_trace=bool(pt.get_option("gen_trace")))
     shade_taps = bool(pt.get_option("shade_taps")) and jit
     if trace_n:  # dominant kernel: the binned trace pass (flops of its passes / their device time)
         hot = ("pt_bin_trace_m_jit" if shade_taps else "pt_bin_trace_jit") if jit else "pt_bin_trace_kernel"

@@ -99,6 +99,7 @@ struct pt_ctx {
     hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {};
     int bin_lanes = -1;                    // pt_set_option "bin_lanes"; -1 = env PT_BIN_LANES
     int shade_taps = -1;                   // pt_set_option "shade_taps"; -1 = env PT_SHADE_TAPS
+    int gen_trace_used = 0;                // the last timed dispatch's first pass made its own camera rays
     int cu_count = 0;
     bool fast_bounds = false;  // every box coordinate inside the reciprocal-division guard
     float bound_k = 0.0f;      // pt_bound_k of the uploaded scene (NaN: no map() bound)
@@ -874,9 +875,11 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             const char *v = std::getenv("PT_GEN_TRACE");
             return v ? std::atoi(v) : 1;
         }();
+        if (!stats) c->gen_trace_used = 0;
         for (int i = 0; i < nl; ++i) {
             if (gen_trace && P[i].gen_order && jit && taps_shade && !stats && jm->trace_g) {
                 P[i].gen_trace = 1;
+                c->gen_trace_used = 1;
             } else if (jit && gen_jit) {
                 void *args[] = {&P[i]};
                 HIPCHK(c, hipModuleLaunchKernel(stats ? jm->gen_stats : jm->gen, item_grid(size_t(P[i].n_src_const)), 1,
@@ -1264,6 +1267,7 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * double(c->n_lanes) * kBinBytesPerSample;
     else if (!std::strcmp(key, "bin_lanes")) *value = double(bin_lanes(c));
     else if (!std::strcmp(key, "shade_taps")) *value = shade_taps(c) ? 1.0 : 0.0;
+    else if (!std::strcmp(key, "gen_trace")) *value = double(c->gen_trace_used);
     else if (!std::strncmp(key, "tap_stat_", 9)) {  // tap_stat_<k>: counter k of the last stats run's shade-pass taps
         const int k = std::atoi(key + 9);
         if (k < 0 || k >= PT_ST_COUNT) return fail(c, PT_ERR_INVALID, "tap_stat index out of range");
