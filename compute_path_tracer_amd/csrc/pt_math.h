@@ -129,6 +129,23 @@ PT_HD float pt_div_rcp(float a, float b, float y) {
     const float r = fmaf(-q, b, a);
     return fmaf(r, y, q);
 }
+// a / b for a constant b, |b| in [2^-4, 2^4], and y = RN(1/b) (the baked
+// scene kernels' scale divisions): pt_div_rcp, then v_div_fixup for a's
+// specials (zeros, infinities, NaN -- the IEEE division ends in the same
+// instruction, so the same results), and the IEEE division for a wave with a
+// finite a outside [2^-60, 2^120) (there an intermediate could leave the
+// normal range).  tests/test_gpu_selftest.py checks it against a / b.
+PT_HD float pt_div_k(float a, float b, float y) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    float q = __builtin_amdgcn_div_fixupf(pt_div_rcp(a, b, y), b, a);
+    const uint32_t e = uint32_t(__builtin_amdgcn_frexp_expf(a) + 59);  // a = m 2^e, m in [0.5, 1); 0 for 0/inf/NaN
+    if (__builtin_expect(__ballot(e > 179u) != 0ull, 0)) q = a / b;
+    return q;
+#else
+    (void)y;
+    return a / b;
+#endif
+}
 // slab operand guard: 0 or |x| in [2^-36, 2^59] (then a difference of two
 // such values is 0 or in [2^-60, 2^60])
 PT_HD bool pt_div_coord_ok(float x) {

@@ -172,7 +172,45 @@ __global__ void box_random(uint32_t seed, uint32_t n, int mode, unsigned long lo
     }
 }
 
+// pt_div_k(a, b, RN(1/b)) against the IEEE a / b, bit for bit, for every a
+// of a slice of the 2^32 patterns (zeros, subnormals, infinities and NaNs
+// included).
+__global__ void divk_sweep(uint32_t a0, float b, unsigned long long *bad, unsigned long long *first) {
+    const uint32_t a_bits = a0 + blockIdx.x * blockDim.x + threadIdx.x;
+    const float a = __uint_as_float(a_bits);
+    volatile float bv = b;  // (no constant folding of the reference division)
+    const float bb = bv;
+    const float y = 1.0f / bb;
+    const float want = a / bb;
+    const float got = pt_div_k(a, bb, y);
+    if (__float_as_uint(got) != __float_as_uint(want)) {
+        atomicAdd(bad, 1ull);
+        atomicMin(first, (unsigned long long)a_bits);
+    }
+}
+
 }  // namespace
+
+extern "C" int pt_check_div_k(int hip_device, float b, uint32_t a0, uint32_t na, uint64_t *mismatches,
+                              uint64_t *first_bad) {
+    if (!mismatches || !first_bad || na % 256u != 0u || a0 + uint64_t(na) > (1ull << 32)) return PT_ERR_INVALID;
+    if (hipSetDevice(hip_device) != hipSuccess) return PT_ERR_HIP;
+    unsigned long long *d = nullptr;
+    if (hipMalloc(&d, 2 * sizeof(*d)) != hipSuccess) return PT_ERR_HIP;
+    const unsigned long long init[2] = {0ull, ~0ull};
+    int rc = hipMemcpy(d, init, sizeof init, hipMemcpyHostToDevice) == hipSuccess ? PT_OK : PT_ERR_HIP;
+    for (uint64_t a = a0; rc == PT_OK && a < uint64_t(a0) + na; a += 1ull << 28) {  // 2^28 per launch
+        const uint64_t cnt = std::min<uint64_t>(1ull << 28, uint64_t(a0) + na - a);
+        hipLaunchKernelGGL(divk_sweep, dim3(unsigned(cnt / 256u)), dim3(256), 0, 0, uint32_t(a), b, d, d + 1);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = PT_ERR_HIP;
+    }
+    unsigned long long h[2] = {0ull, 0ull};
+    if (rc == PT_OK && hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) rc = PT_ERR_HIP;
+    *mismatches = h[0];
+    *first_bad = h[1];
+    (void)hipFree(d);
+    return rc;
+}
 
 extern "C" int pt_check_box_random(int hip_device, uint32_t seed, uint32_t n, int mode, uint64_t *counts) {
     if (!counts) return PT_ERR_INVALID;

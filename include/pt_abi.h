@@ -259,6 +259,10 @@ int pt_check_div_random(int hip_device, uint32_t seed, uint32_t n, uint64_t *mis
  * test, [1]: undecided pairs whose exact fallback differs, [2]: undecided
  * pairs, [3]: pairs drawn outside the guards (skipped). */
 int pt_check_box_random(int hip_device, uint32_t seed, uint32_t n, int mode, uint64_t *counts);
+/* Self-test: pt_div_k(a, b, RN(1/b)) (the baked scene kernels' division by a
+ * scale constant, |b| in [2^-4, 2^4]) against the IEEE a / b, bit for bit,
+ * for the na patterns a0 .. a0 + na - 1 (na a multiple of 256). */
+int pt_check_div_k(int hip_device, float b, uint32_t a0, uint32_t na, uint64_t *mismatches, uint64_t *first_bad);
 
 #ifdef __cplusplus
 }

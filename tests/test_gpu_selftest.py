@@ -106,3 +106,14 @@ def test_margin_decided_slab_test(gpu, mode):
     assert skipped < n // 4
     if mode == 1:
         assert undecided > 0  # the near-ties reach the fallback
+
+
+@pytest.mark.parametrize("b", [1.0 / 0.9, 1.0 / 1.1, 0.9, 1.1, 1.0, 3.0, 0.3, 0.0625, 16.0, -1.25,
+                               1.9999998807907104, 1.0000001192092896])
+def test_div_k_every_numerator(gpu, b):
+    """pt_div_k (the baked kernels' division by a scale constant) equals the
+    IEEE a / b for all 2^32 numerator patterns: the guarded Markstein range,
+    the v_div_fixup specials and the wave fallback."""
+    bad, first = ctypes.c_uint64(), ctypes.c_uint64()
+    assert N.lib().pt_check_div_k(0, ctypes.c_float(b), 0, 0xFFFFFF00, ctypes.byref(bad), ctypes.byref(first)) == N.PT_OK
+    assert bad.value == 0, hex(first.value)
