@@ -133,6 +133,13 @@ __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro,
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// material table entries a map type's shade pass stages in LDS (0: none;
+// the scene kernels specialise it with their table's size, pt_jit.cpp)
+template <class Map>
+struct MapMats {
+    static constexpr int n = 0;
+};
+
 // bounds() of the shade pass, per map type: the generic box loop; the
 // scene kernels specialise it (pt_jit.cpp: straight-line slab tests with
 // constant check[] bits, boxes baked as literals in the tier-up build).
@@ -228,7 +235,19 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
 template <class Map, bool ST, bool TAPS>
 __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
-    hist_zero(lh);
+    // the scene kernels' material table (MapMats<Map>::n entries) staged in
+    // LDS: a hit's material is then one LDS read, not three dependent global
+    // round trips after the taps
+    constexpr int NM = MapMats<Map>::n;
+    __shared__ PtMat lm[NM > 0 ? NM : 1];
+    const PtMat *mats = P.L.mats;
+    if constexpr (NM > 0) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(P.L.mats);
+        uint4 *dst = reinterpret_cast<uint4 *>(lm);
+        for (int k = int(threadIdx.x); k < NM * int(sizeof(PtMat) / 16); k += int(blockDim.x)) dst[k] = src[k];
+        mats = lm;
+    }
+    hist_zero(lh);  // (its barrier also publishes lm)
     Stats<ST> st;
     st.init();
     Stats<ST> stt;  // the normal taps' work (TAPS = false)
@@ -278,7 +297,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             }
             stt.add(PT_ST_NORMAL_MAPS, 6);
         }
-        const bool done = shade_lane<ST>(L.mats, L.bounces, mat, dv0, dv1, dv2, 0, rng, ro, rd, thr, ret, seg, st);
+        const bool done = shade_lane<ST>(mats, L.bounces, mat, dv0, dv1, dv2, 0, rng, ro, rd, thr, ret, seg, st);
         // ret += emission * throughput (test_compute.glsl:148) on the colour
         // slot: 0 + e, added to the slot, equals the slot plus e (a slot
         // never holds -0), and a zero e changes no slot, so only emitting
