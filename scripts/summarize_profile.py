@@ -87,6 +87,12 @@ def main(tag: str, src: str = None) -> None:
         return t[0] if t else None
 
     ktime = avg_s(hot)
+    # bench.py's HIP events time every trace launch, the first pass's
+    # pt_bin_trace_g_jit (own camera rays) included: the launch-weighted
+    # average over both is the figure to compare
+    trace_rows = [r for r in stats if r["Name"] == hot or r["Name"] == "pt_bin_trace_g_jit"]
+    calls = sum(int(r["Calls"]) for r in trace_rows)
+    trace_avg = sum(float(r["TotalDurationNs"]) for r in trace_rows) * 1e-9 / calls if calls else None
     if ktime and "hbm_bytes_per_launch" in d:
         d["hbm_gbs_measured"] = d["hbm_bytes_per_launch"] / ktime / 1e9
     others = {}
@@ -100,6 +106,7 @@ def main(tag: str, src: str = None) -> None:
         others[n] = od
     out = {"tag": tag, "kernel": meta, "per_launch_counters": per_launch, "derived": d,
            "kernel_avg_s_kernel_trace": ktime,
+           "trace_launch_avg_s_kernel_trace": trace_avg,
            "bench_config": bench_line["config"] if bench_line else None,
            "bench_value": bench_line["value"] if bench_line else None,
            "bench_kernel_ms_hip_events": bench_line["roofline"]["kernel_ms_per_launch"] if bench_line else None,
@@ -112,8 +119,10 @@ def main(tag: str, src: str = None) -> None:
              "## Kernel stats", "", "| kernel | calls | avg ms | % |", "|---|---|---|---|"]
     for r in stats:
         lines.append(f"| {r['Name']} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | {float(r['Percentage']):.2f} |")
-    lines += ["", f"HIP-event time of the same kernel inside bench.py: "
-                  f"{out['bench_kernel_ms_hip_events']} ms per launch", "",
+    lines += ["", f"HIP-event time per trace launch inside bench.py: "
+                  f"{out['bench_kernel_ms_hip_events']} ms; rocprofv3 over the same launches "
+                  f"({hot} + pt_bin_trace_g_jit, launch-weighted): "
+                  f"{trace_avg * 1e3 if trace_avg else None} ms", "",
               "## Hot kernel counters (per launch)", "", f"kernel: {meta}", ""]
     for k, v in sorted(per_launch.items()):
         lines.append(f"- {k}: {v:.6g}")
