@@ -477,20 +477,26 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     uint32_t R = n / (gridDim.x * 8u);
     R = R < 64u ? 64u : (R > rmax ? rmax : (R + 63u) & ~63u);
     auto run_len = [&](uint32_t) { return R; };
+#ifdef PT_EXP_STATICRUN  // timing experiment: runs dealt round-robin, no cursor atomics
+    uint32_t run_k = 0u;
+    auto take = [&](uint32_t len) { return (blockIdx.x + (run_k++) * gridDim.x) * len; };
+#else
+    auto take = [&](uint32_t len) { return atomicAdd(&P.ctrl[1], len); };
+#endif
 
     // runs [run_cur, run_end); the next run is reserved one run ahead
     uint32_t nxt = 0u, nxt_len = run_len(0u);
-    if (lane == 0) nxt = atomicAdd(&P.ctrl[1], nxt_len);
+    if (lane == 0) nxt = take(nxt_len);
     uint32_t run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt))), run_end = 0u;
     run_end = run_cur < n ? (run_cur + nxt_len < n ? run_cur + nxt_len : n) : run_cur;
     nxt_len = run_len(run_cur);
-    if (lane == 0 && run_cur < n) nxt = atomicAdd(&P.ctrl[1], nxt_len);
+    if (lane == 0 && run_cur < n) nxt = take(nxt_len);
     auto next_window = [&](uint32_t &b, uint32_t &c) {
         if (run_cur >= run_end) {
             run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt)));
             run_end = run_cur < n ? (run_cur + nxt_len < n ? run_cur + nxt_len : n) : run_cur;
             nxt_len = run_len(run_cur);
-            if (lane == 0 && run_cur < n) nxt = atomicAdd(&P.ctrl[1], nxt_len);
+            if (lane == 0 && run_cur < n) nxt = take(nxt_len);
         }
         b = run_cur;
         c = run_end - run_cur < 64u ? run_end - run_cur : 64u;
