@@ -133,6 +133,19 @@ __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro,
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// check[] wider than 64 bits, per map type: -1 = decided at run time
+// (PtPass.wide); the scene kernels specialise it with their scene's answer,
+// so a narrow scene's kernels carry no high mask words at all
+template <class Map>
+struct MapWide {
+    static constexpr int v = -1;
+};
+template <class Map>
+__device__ __forceinline__ bool wide_of(const PtPass &P) {
+    if constexpr (MapWide<Map>::v >= 0) return MapWide<Map>::v != 0;
+    else return P.wide != 0;
+}
+
 // material table entries a map type's shade pass stages in LDS (0: none;
 // the scene kernels specialise it with their table's size, pt_jit.cpp)
 template <class Map>
@@ -207,7 +220,7 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
         store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, rng, i, 0u, make_uint4(m.x, m.y, 0u, 0u));
         P.color[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the path's radiance (ret) starts at 0
-        if (P.wide) P.mask_hi[i] = make_uint2(m.z, m.w);
+        if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         if (!P.gen_order) {
             const uint32_t b = bin_of(m);
             P.key[i] = b;
@@ -321,7 +334,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         }
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
         store_ray(P.rin + i, ro, rd, thr, rng, sid, 0u, make_uint4(m.x, m.y, 0u, 0u));
-        if (P.wide) P.mask_hi[i] = make_uint2(m.z, m.w);
+        if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);
         P.key[i] = k;
         atomicAdd(&lh[k], 1u);
@@ -332,7 +345,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint4 q0 = P.rin[i].q[0], q1 = P.rin[i].q[1], q2 = P.rin[i].q[2], q3 = P.rin[i].q[3];
         uint2 hi = make_uint2(0u, 0u);
-        if (!TAPS && P.wide) {
+        if (!TAPS && wide_of<Map>(P)) {
             const float4 nd = P.hitn[i];
             hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
         }
@@ -463,7 +476,7 @@ template <class Map, bool ST, bool TAPS = true, bool GEN = false>
 __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     // the staged window, once its loads have landed: [part][lane], so a
     // refill reads a ray with 4 ds_read_b128 instead of 16 cross-lane moves
-    __shared__ uint4 W[5][64];
+    __shared__ uint4 W[MapWide<Map>::v == 0 ? 4 : 5][64];  // (W[4]: check[] bits 64..127)
     const PtLaunch &L = P.L;
     const int lane = int(threadIdx.x);
     Stats<ST> st;
@@ -539,7 +552,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             s1 = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w));
             s2 = make_float4(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w));
             s3 = v[3];
-            if (P.wide) sh = P.mask_hi[nslot];
+            if (wide_of<Map>(P)) sh = P.mask_hi[nslot];
         }
         if (wcnt != 0u) {
             next_window(nb, nc);
@@ -576,7 +589,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 const bool in_win = uint32_t(lane) < wcnt;
                 ck.alo = wave_or_u64((mapping_now ? ck.lo : 0ull) |
                                      (in_win ? (uint64_t(s3.x) | (uint64_t(s3.y) << 32)) : 0ull));
-                ck.ahi = P.wide ? wave_or_u64((mapping_now ? ck.hi : 0ull) |
+                ck.ahi = wide_of<Map>(P) ? wave_or_u64((mapping_now ? ck.hi : 0ull) |
                                               (in_win ? (uint64_t(sh.x) | (uint64_t(sh.y) << 32)) : 0ull))
                                 : 0ull;
                 W[0][lane] = make_uint4(__float_as_uint(s0.x), __float_as_uint(s0.y), __float_as_uint(s0.z),
@@ -586,7 +599,8 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 W[2][lane] = make_uint4(__float_as_uint(s2.x), __float_as_uint(s2.y), __float_as_uint(s2.z),
                                         __float_as_uint(s2.w));
                 W[3][lane] = s3;
-                if (P.wide) W[4][lane] = make_uint4(sh.x, sh.y, 0u, 0u);
+                if constexpr (MapWide<Map>::v != 0)
+                    if (wide_of<Map>(P)) W[4][lane] = make_uint4(sh.x, sh.y, 0u, 0u);
                 in_lds = true;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
@@ -604,10 +618,12 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 c0 = __uint_as_float(wc.x), c1 = __uint_as_float(wc.y), c2 = __uint_as_float(wc.z);
                 c3 = __uint_as_float(wc.w);
                 d0 = wd.x, d1 = wd.y, d2 = wd.z, d3 = wd.w;
-                if (P.wide) {
-                    const uint4 we = W[4][src];
-                    e0 = we.x;
-                    e1 = we.y;
+                if constexpr (MapWide<Map>::v != 0) {
+                    if (wide_of<Map>(P)) {
+                        const uint4 we = W[4][src];
+                        e0 = we.x;
+                        e1 = we.y;
+                    }
                 }
             }
             if (got) {
@@ -675,7 +691,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 } else {  // hit point + check[] + tap bound + material (bin_shade_body)
                     store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
                               make_uint4(uint32_t(ck.lo), uint32_t(ck.lo >> 32), __float_as_uint(dv0), 0u));
-                    if (P.wide)
+                    if (wide_of<Map>(P))
                         P.hitn[pos] = make_float4(0.0f, 0.0f, __uint_as_float(uint32_t(ck.hi)),
                                                   __uint_as_float(uint32_t(ck.hi >> 32)));
                 }
