@@ -789,12 +789,12 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     const unsigned trace_grid = cu * unsigned(std::max(1, per_cu));
     static const int run_max = [] {  // A/B knob
         const char *v = std::getenv("PT_BIN_RUN");
-        const int r = v ? std::atoi(v) : 256;
+        const int r = v ? std::atoi(v) : 512;
         return r >= 64 ? (r / 64) * 64 : 256;
     }();
     static const int refill_min = [] {  // A/B knob
         const char *v = std::getenv("PT_REFILL_MIN");
-        const int r = v ? std::atoi(v) : 4;
+        const int r = v ? std::atoi(v) : 2;
         return r >= 1 && r <= 64 ? r : 4;
     }();
     static const unsigned shade_cu_env = [] {  // A/B knob: shade blocks per CU
