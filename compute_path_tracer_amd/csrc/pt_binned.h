@@ -417,10 +417,20 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
     // the places with LDS cursors.
     const uint32_t per = ((n + gridDim.x - 1u) / gridDim.x + PT_BIN_BLOCK - 1u) & ~uint32_t(PT_BIN_BLOCK - 1);
     const uint32_t b0 = min(n, blockIdx.x * per), b1 = min(n, b0 + per);
+    // (eight keys in flight per thread: the loads are issued before the LDS
+    // atomics that use them)
+    constexpr uint32_t U = 8u;
     hist_zero(cnt);
-    for (uint32_t e = b0 + threadIdx.x; e < b1; e += PT_BIN_BLOCK) {
-        const uint32_t k = P.key[e];
-        if (k != PT_BIN_NONE) atomicAdd(&cnt[k], 1u);
+    for (uint32_t e0 = b0 + threadIdx.x; e0 < b1; e0 += U * PT_BIN_BLOCK) {
+        uint32_t k[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) {
+            const uint32_t e = e0 + j * PT_BIN_BLOCK;
+            k[j] = e < b1 ? P.key[e] : PT_BIN_NONE;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j)
+            if (k[j] != PT_BIN_NONE) atomicAdd(&cnt[k[j]], 1u);
     }
     __syncthreads();
     for (int b = int(threadIdx.x); b < PT_BINS; b += PT_BIN_BLOCK) {
@@ -428,9 +438,16 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
         if (c != 0u) cnt[b] = atomicAdd(&P.offs[b], c);
     }
     __syncthreads();
-    for (uint32_t e = b0 + threadIdx.x; e < b1; e += PT_BIN_BLOCK) {
-        const uint32_t k = P.key[e];
-        if (k != PT_BIN_NONE) P.idx[atomicAdd(&cnt[k], 1u)] = e;
+    for (uint32_t e0 = b0 + threadIdx.x; e0 < b1; e0 += U * PT_BIN_BLOCK) {
+        uint32_t k[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) {
+            const uint32_t e = e0 + j * PT_BIN_BLOCK;
+            k[j] = e < b1 ? P.key[e] : PT_BIN_NONE;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j)
+            if (k[j] != PT_BIN_NONE) P.idx[atomicAdd(&cnt[k[j]], 1u)] = e0 + j * PT_BIN_BLOCK;
     }
     return;
 #endif
