@@ -283,7 +283,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             // (the taps' counters go to their own half of the stats buffer:
             // pt_dispatch_stats sums both, bench.py splits the flops by pass)
             // hit record: q3 = {check[] bits 0..63, tap bound}, hi = check[] bits 64..127
-            const Check ck{uint64_t(q3.x) | (uint64_t(q3.y) << 32), uint64_t(hi.x) | (uint64_t(hi.y) << 32)};
+            Check ck{uint64_t(q3.x) | (uint64_t(q3.y) << 32), uint64_t(hi.x) | (uint64_t(hi.y) << 32)};
             const float bnd = __uint_as_float(q3.z);
             // bnd widened by the taps' spread (two taps are at most 2e apart,
             // plus their coordinates' rounding): the first tap's tests against
@@ -299,6 +299,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                     if (first_active_lane()) stt.add(PT_ST_WAVE_MAPS);
                 const Hit h = k == 0 ? Map::template first<ST>(L, qx, qy, qz, ck, bnd, bndw, live, stt)
                                      : Map::template rest<ST>(L, qx, qy, qz, ck, bnd, bndw, live, stt);
+                if (k == 0) ck.alo = Map::alive(live);  // (the other taps' wave-level live test)
                 if ((k & 1) == 0) {
                     dp = h.d;  // d(p + e)
                 } else {
