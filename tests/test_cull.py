@@ -194,3 +194,29 @@ def test_far_box_takes_the_ieee_bounds_path(tmp_path):
     assert "const bool fast = false && " in src
     src_c2, _ = _baked("c2", tmp_path)
     assert "const bool fast = true && " in src_c2
+
+
+@pytest.mark.parametrize("scene,wide", [("c3", 0), ("wide", 1)])
+def test_check_width_is_a_compile_time_constant(scene, wide, tmp_path):
+    """MapWide: a scene whose check[] indices stay below 64 gets kernels
+    without the high mask words; a wider one keeps them (pt_jit.cpp)."""
+    src, _ = _baked(scene, tmp_path)
+    for m in ("JitMap", "JitTaps"):
+        assert f"template <> struct MapWide<{m}> {{\n  static constexpr int v = {wide};" in src
+
+
+def test_material_table_size_and_scale_reciprocals(tmp_path):
+    """The shade pass's LDS material table covers every material a shape can
+    name, and each baked scale division uses the correctly rounded reciprocal
+    of its divisor (pt_div_k)."""
+    src, nodes = _baked("c3", tmp_path)
+    prog = scenes.SCENES["c3"]().compile(CompData())
+    n_mat = int(re.search(r"struct MapMats<JitTaps> \{\n  static constexpr int n = (\d+);", src).group(1))
+    shapes = [m for m in re.finditer(r"constexpr PtNode B\d+\{1, \d+, \d+, -?\d+, (\d+),", src[:src.index("struct JitMapB")])]
+    assert n_mat == 1 + max(int(m.group(1)) for m in shapes)
+    calls = re.findall(r"pt_div_k\(d, B(\d+)\.inv, ([^)]+)\)", src)
+    assert calls, "C3's scaled unions divide by their scale constants"
+    for i, y in calls:
+        inv = np.float32(nodes[int(i)]["inv"])
+        assert np.float32(_value(y)) == np.float32(1.0) / inv
+    assert prog.n_ops > 0
