@@ -785,7 +785,10 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     // default: leave one wave slot per SIMD (4 per CU) to the other pipeline,
     // so its shade / scatter / scan blocks run beside the persistent trace
     // waves instead of waiting for a pass to drain (24 of 28: +1.5 %)
-    else if (trace_cu_env == 0 && per_cu > 8) per_cu -= 4;
+    else if (trace_cu_env == 0 && per_cu > 8) per_cu = std::min(per_cu - 4, 24);
+    // (at most 6 per SIMD: with the 64-VGPR narrow-scene kernel, 7 left the
+    // other pipeline's one-wave scan waiting ~1.7 ms per pass; 24 vs 28:
+    // +1.5 %)
     const unsigned trace_grid = cu * unsigned(std::max(1, per_cu));
     static const int run_max = [] {  // A/B knob
         const char *v = std::getenv("PT_BIN_RUN");
