@@ -607,6 +607,11 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 const bool in_win = uint32_t(lane) < wcnt;
                 ck.alo = wave_or_u64((mapping_now ? ck.lo : 0ull) |
                                      (in_win ? (uint64_t(s3.x) | (uint64_t(s3.y) << 32)) : 0ull));
+#ifdef PT_JIT_AAND_ON
+                // and the bits all of them share: AND = ~OR(~m) (lanes outside add 0)
+                ck.aand = ~wave_or_u64((mapping_now ? ~ck.lo : 0ull) |
+                                       (in_win ? ~(uint64_t(s3.x) | (uint64_t(s3.y) << 32)) : 0ull));
+#endif
                 ck.ahi = wide_of<Map>(P) ? wave_or_u64((mapping_now ? ck.hi : 0ull) |
                                               (in_win ? (uint64_t(sh.x) | (uint64_t(sh.y) << 32)) : 0ull))
                                 : 0ull;

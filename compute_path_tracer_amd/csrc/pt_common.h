@@ -39,6 +39,9 @@ struct Check {  // check[] of the generated bounds(), one bit per entry
     // this mask, wave-uniform (scene kernels test it first: a shape no lane
     // needs is skipped by a scalar branch); all ones = no information
     uint64_t alo = ~0ull, ahi = ~0ull;
+    // a subset of the check[] bits every such lane has (bits 0..63; 0 = no
+    // information): a shape set here needs no lane test
+    uint64_t aand = 0ull;
 };
 // a lane's check[] bit behind the wave-uniform test of Check.alo/ahi: the
 // empty volatile asm keeps the compiler from merging the two tests into one
