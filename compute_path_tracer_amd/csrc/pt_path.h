@@ -72,6 +72,30 @@ __device__ __forceinline__ bool ray_box_approx(const PtAabb &bx, float ox, float
     return tnear < tfar && tfar > 0.0f;
 }
 
+// The slab test from one fma per slab: t' = RN(b * y + n) with n = -RN(o * y)
+// per ray and axis, y = RN(1/d).  Under the guards of ray_box_rcp,
+// |t' - t| <= 2^-21 |t| + 2^-23 M for every slab value t = RN(RN(b - o) / d),
+// M = max over the axes of |n| (the product's rounding adds an absolute
+// term: DESIGN.md 3.18).  `gap` as in ray_box_approx and `tfa` (the least
+// |tfar'|) decide a lane when gap > 2^-21 M and tfa > 2^-22 M (fma_decided);
+// an undecided lane takes ray_box_rcp.  One fma per slab instead of a
+// subtraction and a product.
+__device__ __forceinline__ bool ray_box_fma(const PtAabb &bx, float nx, float ny, float nz, float yx, float yy,
+                                            float yz, float &gap, float &tfa) {
+    const float tminx = fmaf(bx.bmin[0], yx, nx), tmaxx = fmaf(bx.bmax[0], yx, nx);
+    const float tminy = fmaf(bx.bmin[1], yy, ny), tmaxy = fmaf(bx.bmax[1], yy, ny);
+    const float tminz = fmaf(bx.bmin[2], yz, nz), tmaxz = fmaf(bx.bmax[2], yz, nz);
+    const float tnear = pt_gmax(pt_gmax(pt_gmin(tminx, tmaxx), pt_gmin(tminy, tmaxy)), pt_gmin(tminz, tmaxz));
+    const float tfar = pt_gmin(pt_gmin(pt_gmax(tminx, tmaxx), pt_gmax(tminy, tmaxy)), pt_gmax(tminz, tmaxz));
+    gap = fminf(gap, fabsf(tfar - tnear) - (fabsf(tnear) + fabsf(tfar)) * 0x1p-20f);
+    tfa = fminf(tfa, fabsf(tfar));
+    return tnear < tfar && tfar > 0.0f;
+}
+__device__ __forceinline__ bool fma_decided(float gap, float tfa, float nx, float ny, float nz) {
+    const float m = pt_gmax(fabsf(nx), pt_gmax(fabsf(ny), fabsf(nz)));
+    return gap > m * 0x1p-21f && tfa > m * 0x1p-22f;
+}
+
 // The map() argument of a lane: CastRay's p = ro + rd*t (MARCH), or normal
 // tap `step` (0..5 = +x,-x,+y,-y,+z,-z) around the hit point held in ro
 // (calc_normal, test_compute.glsl:57-66).
