@@ -1022,10 +1022,10 @@ static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, u
     if (L.kernel == PT_KERNEL_AUTO) {
         // small dispatches take the tile-resident wave kernel: one launch, no
         // pass sequence and no per-pass tails.  Crossover measured at about
-        // samples x ops = 2^26 (scripts/kernel_crossover.py: C1 3x faster at
+        // samples x ops = 2^27 (scripts/kernel_crossover.py: C1 3x faster at
         // 65 K samples; the 32-node scene binned from ~4 M samples on)
         const double work = double(L.n_tiles) * 64.0 * double(spp) * double(std::max<size_t>(1, c->ops.size()));
-        L.kernel = work < 67108864.0 ? PT_KERNEL_WAVEFRONT : PT_KERNEL_BINNED;
+        L.kernel = work < 134217728.0 ? PT_KERNEL_WAVEFRONT : PT_KERNEL_BINNED;
     }
     L.shade_batch = c->shade_batch > 0 ? c->shade_batch : (env_batch > 0 ? env_batch : 16);  // measured best
     return PT_OK;
