@@ -105,21 +105,21 @@ __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro,
     if (fast) {
         const float yx = 1.0f / rd.x, yy = 1.0f / rd.y, yz = 1.0f / rd.z;
         // slab values from the reciprocal products; a wave with an undecided
-        // comparison redoes every box exactly (ray_box_approx)
-        float gap = __builtin_inff();
+        // comparison redoes every box exactly (ray_box_ulp)
+        uint32_t gapu = 0xffffffffu;
 #pragma unroll 4  // scalar box loads issued ahead of their slab tests
         for (int b = 0; b < L.n_aabb; ++b) {
             const PtAabb bx = boxes[b];
-            if (ray_box_approx(bx, ro.x, ro.y, ro.z, yx, yy, yz, gap)) w[bx.back >> 5] |= 1u << (bx.back & 31);
+            if (ray_box_ulp(bx, ro.x, ro.y, ro.z, yx, yy, yz, gapu)) w[bx.back >> 5] |= 1u << (bx.back & 31);
         }
-        if (__builtin_expect(__ballot(!(gap > 0.0f)) != 0ull, 0)) {
+        if (__builtin_expect(__ballot(!(gapu > PT_ULP_MARGIN)) != 0ull, 0)) {
             uint32_t v[4] = {0u, 0u, 0u, 0u};
             for (int b = 0; b < L.n_aabb; ++b) {
                 const PtAabb bx = boxes[b];
                 if (ray_box_rcp(bx, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, yx, yy, yz))
                     v[bx.back >> 5] |= 1u << (bx.back & 31);
             }
-            if (!(gap > 0.0f))
+            if (!(gapu > PT_ULP_MARGIN))
                 for (int k = 0; k < 4; ++k) w[k] = v[k];
         }
     } else {
@@ -333,7 +333,16 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             P.key[i] = PT_BIN_NONE;
             return;
         }
-        const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
+        uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
+#ifdef PT_EXP_BOUNDS2  // timing experiment: bounds() twice (the marginal cost of its slab tests)
+        {
+            pt_f3 o2 = ro;
+            __asm__ volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+            const uint4 m2 = MapBounds<Map>::template mask<ST>(L, o2, rd, st);
+            m.x |= m2.x;  // (the same bits; the compiler cannot tell)
+            m.y |= m2.y;
+        }
+#endif
         store_ray(P.rin + i, ro, rd, thr, rng, sid, 0u, make_uint4(m.x, m.y, 0u, 0u));
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);

@@ -72,6 +72,32 @@ __device__ __forceinline__ bool ray_box_approx(const PtAabb &bx, float ox, float
     return tnear < tfar && tfar > 0.0f;
 }
 
+// ray_box_approx with the margin in units of the last place (DESIGN.md
+// 3.19): each slab value t' is within 4 representable steps of the IEEE slab
+// value (3 roundings of <= 2^-24 relative each), with the same sign and
+// zeros, so min / max keep tnear' and tfar' within 4 steps of the IEEE tnear
+// and tfar, and tnear' < tfar' decides tnear < tfar whenever the two bit
+// patterns differ by more than 8 (opposite signs differ by >= 2^31 and are
+// decided by the signs).  `gapu` keeps the least |bits(tfar') -
+// bits(tnear')| (v_sad_u32: one instruction, against four for the float
+// margin); a lane whose gapu is <= PT_ULP_MARGIN takes ray_box_rcp.
+#define PT_ULP_MARGIN 16u
+__device__ __forceinline__ uint32_t pt_absdiff_u32(uint32_t a, uint32_t b) {
+    uint32_t d;
+    __asm__("v_sad_u32 %0, %1, %2, 0" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+__device__ __forceinline__ bool ray_box_ulp(const PtAabb &bx, float ox, float oy, float oz, float yx, float yy,
+                                            float yz, uint32_t &gapu) {
+    const float tminx = (bx.bmin[0] - ox) * yx, tmaxx = (bx.bmax[0] - ox) * yx;
+    const float tminy = (bx.bmin[1] - oy) * yy, tmaxy = (bx.bmax[1] - oy) * yy;
+    const float tminz = (bx.bmin[2] - oz) * yz, tmaxz = (bx.bmax[2] - oz) * yz;
+    const float tnear = pt_gmax(pt_gmax(pt_gmin(tminx, tmaxx), pt_gmin(tminy, tmaxy)), pt_gmin(tminz, tmaxz));
+    const float tfar = pt_gmin(pt_gmin(pt_gmax(tminx, tmaxx), pt_gmax(tminy, tmaxy)), pt_gmax(tminz, tmaxz));
+    gapu = min(gapu, pt_absdiff_u32(__float_as_uint(tfar), __float_as_uint(tnear)));
+    return tnear < tfar && tfar > 0.0f;
+}
+
 // The slab test from one fma per slab: t' = RN(b * y + n) with n = -RN(o * y)
 // per ray and axis, y = RN(1/d).  Under the guards of ray_box_rcp,
 // |t' - t| <= 2^-21 |t| + 2^-23 M for every slab value t = RN(RN(b - o) / d),

@@ -123,7 +123,9 @@ __global__ void div_random(uint32_t seed, uint32_t n, unsigned long long *bad, u
 // margin must leave undecided.  Modes 2 / 3: the same pairs through the
 // one-fma slabs (ray_box_fma); modes 4 / 5: those with the
 // origin 64x farther out and the box 100x closer along the ray (the fma
-// form's absolute error term at its largest next to the slab values).  Counts: [0] decided lanes whose answer differs
+// form's absolute error term at its largest next to the slab values); modes
+// 6 / 7: the pairs of modes 0 / 1 through the ulp-margin test (ray_box_ulp,
+// DESIGN.md 3.19).  Counts: [0] decided lanes whose answer differs
 // from the IEEE slab test, [1] undecided lanes whose exact answer
 // (ray_box_rcp) differs, [2] undecided lanes, [3] pairs outside the guards.
 __global__ void box_random(uint32_t seed, uint32_t n, int mode, unsigned long long *cnt) {
@@ -132,7 +134,7 @@ __global__ void box_random(uint32_t seed, uint32_t n, int mode, unsigned long lo
     uint32_t h = mix32(seed ^ mix32(i * 16u + 1u));
     auto next = [&]() { return h = mix32(h + 0x9E3779B9u); };
     float o[3], d[3], p[3];
-    const bool far = mode >= 4;
+    const bool far = mode == 4 || mode == 5;
     const float t = far ? 0.005f + float(next() >> 8) * (0.16f / 16777216.0f)
                         : 0.5f + float(next() >> 8) * (16.0f / 16777216.0f);
     for (int k = 0; k < 3; ++k) {
@@ -149,7 +151,7 @@ __global__ void box_random(uint32_t seed, uint32_t n, int mode, unsigned long lo
         b.bmin[k] = p[k] - r1;
         b.bmax[k] = p[k] + r2;
     }
-    if (mode == 1 || mode == 3 || mode == 5) {  // entry through face a1 and exit through face a2 at p, jittered by a few ulps
+    if (mode == 1 || mode == 3 || mode == 5 || mode == 7) {  // entry through face a1 and exit through face a2 at p, jittered by a few ulps
         const int a1 = int(next() % 3u), a2 = (a1 + 1 + int(next() % 2u)) % 3;
         const int u1 = int(next() % 9u) - 4, u2 = int(next() % 9u) - 4;
         if (d[a1] > 0.0f) b.bmin[a1] = __uint_as_float(__float_as_uint(p[a1]) + uint32_t(u1));
@@ -168,7 +170,11 @@ __global__ void box_random(uint32_t seed, uint32_t n, int mode, unsigned long lo
     const float yx = 1.0f / d[0], yy = 1.0f / d[1], yz = 1.0f / d[2];
     float gap = __builtin_inff();
     bool approx, decided;
-    if (mode >= 2) {  // the one-fma slabs (ray_box_fma)
+    if (mode >= 6) {  // the ulp margin (ray_box_ulp)
+        uint32_t gapu = 0xffffffffu;
+        approx = pt::ray_box_ulp(b, o[0], o[1], o[2], yx, yy, yz, gapu);
+        decided = gapu > PT_ULP_MARGIN;
+    } else if (mode >= 2) {  // the one-fma slabs (ray_box_fma)
         const float nx = -(o[0] * yx), ny = -(o[1] * yy), nz = -(o[2] * yz);
         float tfa = __builtin_inff();
         approx = pt::ray_box_fma(b, nx, ny, nz, yx, yy, yz, gap, tfa);

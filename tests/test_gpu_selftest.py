@@ -92,10 +92,11 @@ def test_div_rcp_on_guarded_operands(gpu, seed):
     assert bad.value == 0, hex(first.value)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_margin_decided_slab_test(gpu, mode):
     """bounds()' slab test from reciprocal products (modes
-    2-5: one fma per slab, 3.18, 4-5 with far origins and near boxes): every
+    2-5: one fma per slab, 3.18, 4-5 with far origins and near boxes; 6-7:
+    the margin in units of the last place, 3.19): every
     pair the margin decides agrees with the IEEE slab test; the undecided ones
     (ray through a box edge, odd modes) agree after the exact fallback."""
     counts = (ctypes.c_uint64 * 4)()
