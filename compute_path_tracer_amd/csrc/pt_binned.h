@@ -110,7 +110,7 @@ __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro,
 #pragma unroll 4  // scalar box loads issued ahead of their slab tests
         for (int b = 0; b < L.n_aabb; ++b) {
             const PtAabb bx = boxes[b];
-            if (ray_box_ulp(bx, ro.x, ro.y, ro.z, yx, yy, yz, gapu)) w[bx.back >> 5] |= 1u << (bx.back & 31);
+            if (ray_box_ulp<false>(bx, ro.x, ro.y, ro.z, yx, yy, yz, gapu)) w[bx.back >> 5] |= 1u << (bx.back & 31);
         }
         if (__builtin_expect(__ballot(!(gapu > PT_ULP_MARGIN)) != 0ull, 0)) {
             uint32_t v[4] = {0u, 0u, 0u, 0u};

@@ -82,11 +82,16 @@ __device__ __forceinline__ bool ray_box_approx(const PtAabb &bx, float ox, float
 // bits(tnear')| (v_sad_u32: one instruction, against four for the float
 // margin); a lane whose gapu is <= PT_ULP_MARGIN takes ray_box_rcp.
 #define PT_ULP_MARGIN 16u
+// (SAD false: max - min, for loops the compiler is to unroll -- inline asm is
+// convergent, which blocks a runtime-count unroll)
+template <bool SAD = true>
 __device__ __forceinline__ uint32_t pt_absdiff_u32(uint32_t a, uint32_t b) {
+    if constexpr (!SAD) return max(a, b) - min(a, b);
     uint32_t d;
     __asm__("v_sad_u32 %0, %1, %2, 0" : "=v"(d) : "v"(a), "v"(b));
     return d;
 }
+template <bool SAD = true>
 __device__ __forceinline__ bool ray_box_ulp(const PtAabb &bx, float ox, float oy, float oz, float yx, float yy,
                                             float yz, uint32_t &gapu) {
     const float tminx = (bx.bmin[0] - ox) * yx, tmaxx = (bx.bmax[0] - ox) * yx;
@@ -94,8 +99,22 @@ __device__ __forceinline__ bool ray_box_ulp(const PtAabb &bx, float ox, float oy
     const float tminz = (bx.bmin[2] - oz) * yz, tmaxz = (bx.bmax[2] - oz) * yz;
     const float tnear = pt_gmax(pt_gmax(pt_gmin(tminx, tmaxx), pt_gmin(tminy, tmaxy)), pt_gmin(tminz, tmaxz));
     const float tfar = pt_gmin(pt_gmin(pt_gmax(tminx, tmaxx), pt_gmax(tminy, tmaxy)), pt_gmax(tminz, tmaxz));
-    gapu = min(gapu, pt_absdiff_u32(__float_as_uint(tfar), __float_as_uint(tnear)));
+#ifdef PT_ULP_MED3
+    // tnear < tfar && tfar > 0 as one compare, max(tnear, 0) < tfar, with the
+    // 0 folded into each axis as med3(tmin, tmax, 0): it equals max(min(tmin,
+    // tmax), 0) unless both values are negative, and then max(tmin, tmax) < 0
+    // bounds tfar from above and below tnear0 alike (a miss either way).  The
+    // med3 is monotone in each value, so the ulp argument carries over.
+    const float tnear0 = pt_gmax(pt_gmax(__builtin_amdgcn_fmed3f(tminx, tmaxx, 0.0f),
+                                         __builtin_amdgcn_fmed3f(tminy, tmaxy, 0.0f)),
+                                 __builtin_amdgcn_fmed3f(tminz, tmaxz, 0.0f));
+    (void)tnear;
+    gapu = min(gapu, pt_absdiff_u32<SAD>(__float_as_uint(tfar), __float_as_uint(tnear0)));
+    return tnear0 < tfar;
+#else
+    gapu = min(gapu, pt_absdiff_u32<SAD>(__float_as_uint(tfar), __float_as_uint(tnear)));
     return tnear < tfar && tfar > 0.0f;
+#endif
 }
 
 // The slab test from one fma per slab: t' = RN(b * y + n) with n = -RN(o * y)
