@@ -310,6 +310,27 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                 }
             }
             stt.add(PT_ST_NORMAL_MAPS, 6);
+#ifdef PT_EXP_TAPS2  // timing experiment: the six taps twice (the marginal cost of the taps)
+            {
+                pt_f3 r2 = ro;
+                __asm__ volatile("" : "+v"(r2.x), "+v"(r2.y), "+v"(r2.z));
+                Check ck2{uint64_t(q3.x) | (uint64_t(q3.y) << 32), uint64_t(hi.x) | (uint64_t(hi.y) << 32)};
+                uint64_t live2 = 0ull;
+                float dp2 = 0.0f;
+                uint32_t acc = 0u;
+#pragma unroll 1
+                for (int k = 0; k < 6; ++k) {
+                    float qx, qy, qz;
+                    map_point(ST_NORMAL, k, r2, rd, 0.0f, qx, qy, qz);
+                    const Hit h = k == 0 ? Map::template first<ST>(L, qx, qy, qz, ck2, bnd, bndw, live2, stt)
+                                         : Map::template rest<ST>(L, qx, qy, qz, ck2, bnd, bndw, live2, stt);
+                    if (k == 0) ck2.alo = Map::alive(live2);
+                    if ((k & 1) == 0) dp2 = h.d;
+                    else acc |= __float_as_uint(dp2 - h.d) ^ __float_as_uint(k == 1 ? dv0 : (k == 3 ? dv1 : dv2));
+                }
+                dv0 = __uint_as_float(__float_as_uint(dv0) | acc);  // (acc = 0: the same differences)
+            }
+#endif
         }
         const bool done = shade_lane<ST>(mats, L.bounces, mat, dv0, dv1, dv2, 0, rng, ro, rd, thr, ret, seg, st);
         // ret += emission * throughput (test_compute.glsl:148) on the colour
