@@ -24,7 +24,12 @@ for name in names:
     pt = PathTracer(w, h, prog, settings=st)
     pt.set_option("jit_wait", 1)  # setup: the values-baked scene kernel, as bench.py
     aspect = float(np.float32(w) / np.float32(h))
-    pt.dispatch(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), min(spp, 4))  # warm-up
+    # warm-up with the timed dispatch's own spp: the same kernel choice, and
+    # the binned pipeline's chunk buffers (sized by the dispatch's samples,
+    # up to 81.6 GB) allocated before timing -- a smaller warm-up left their
+    # allocation, or the first launch of the binned kernels, inside the timed
+    # dispatch (r02s: C2 at 68-5000 Msamples/s from box to box)
+    pt.dispatch(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), spp)
     pt.sync()
     pt.clear()
     t0 = time.perf_counter()
