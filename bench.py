@@ -130,6 +130,8 @@ def schedule_metrics(st_all: dict, taps: dict) -> dict:
         out["idle_shade"] = round(st["idle_shade"] / (64.0 * st["wave_iters"]), 4)
         out["idle_free"] = round(st["idle_free"] / (64.0 * st["wave_iters"]), 4)
         out["maps_per_sample"] = round(maps / max(1, st["samples"]), 2)
+    if st_all.get("bounds_waves"):  # bounds()' waves that redid every box exactly (an undecided lane)
+        out["bounds_exact_waves"] = round(st_all.get("bounds_exact", 0) / st_all["bounds_waves"], 5)
     if st.get("cyc_total"):  # share of wave time per phase (instrumented kernel)
         out["wave_time"] = {k: round(st["cyc_" + k] / st["cyc_total"], 4)
                             for k in ("refill", "bounds", "map", "shade")}

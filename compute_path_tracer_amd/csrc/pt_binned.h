@@ -103,6 +103,8 @@ __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro,
     const bool fast = L.fast_bounds != 0 && pt_div_coord_ok(ro.x) && pt_div_coord_ok(ro.y) &&
                       pt_div_coord_ok(ro.z) && pt_div_dir_ok(rd.x) && pt_div_dir_ok(rd.y) && pt_div_dir_ok(rd.z);
     if (fast) {
+        if constexpr (ST)
+            if (first_active_lane()) st.add(PT_ST_BOUNDS_WAVES);
         const float yx = 1.0f / rd.x, yy = 1.0f / rd.y, yz = 1.0f / rd.z;
         // slab values from the reciprocal products; a wave with an undecided
         // comparison redoes every box exactly (ray_box_ulp)
@@ -113,6 +115,8 @@ __device__ __forceinline__ uint4 bounds_mask(const PtLaunch &L, const pt_f3 &ro,
             if (ray_box_ulp<false>(bx, ro.x, ro.y, ro.z, yx, yy, yz, gapu)) w[bx.back >> 5] |= 1u << (bx.back & 31);
         }
         if (__builtin_expect(__ballot(!(gapu > PT_ULP_MARGIN)) != 0ull, 0)) {
+            if constexpr (ST)
+                if (first_active_lane()) st.add(PT_ST_BOUNDS_EXACT);
             uint32_t v[4] = {0u, 0u, 0u, 0u};
             for (int b = 0; b < L.n_aabb; ++b) {
                 const PtAabb bx = boxes[b];

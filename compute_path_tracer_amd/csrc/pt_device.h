@@ -96,6 +96,8 @@ enum {
     PT_ST_CYC_TOTAL,    //   whole wave
     PT_ST_CULLED,       // lane shape evaluations dropped by the distance bound (counted in the kinds above too)
     PT_ST_WAVE_EVALS,   // wave-level shape evaluations that ran (WAVE_SHAPES minus whole-wave culls)
+    PT_ST_BOUNDS_WAVES, // waves that ran bounds()' fast slab tests (first active lane counts)
+    PT_ST_BOUNDS_EXACT, // of those, waves with an undecided lane, which redid every box exactly
     PT_ST_COUNT
 };
 
