@@ -188,6 +188,17 @@ __device__ __forceinline__ float sdf_k(const PtNode &n, float x, float y, float 
         const float s = n.size[0];
         const float ax = fabsf(x), ay = fabsf(y), az = fabsf(z);
         const float m = ax + ay + az - s;
+#if (defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)) && defined(PT_OCT_SELECT)
+        // the same values by selects: no exec-mask regions for the branches
+        const bool c1 = 3.0f * ax < m, c2 = 3.0f * ay < m, c3 = 3.0f * az < m;
+        const float q0 = c1 ? ax : (c2 ? ay : az);
+        const float q1 = c1 ? ay : (c2 ? az : ax);
+        const float q2 = c1 ? az : (c2 ? ax : ay);
+        const float k = pt_gmin(pt_gmax(0.5f * (q2 - q1 + s), 0.0f), s);
+        const float vy = q1 - s + k, vz = q2 - k;
+        const float len = pt_sqrt(q0 * q0 + vy * vy + vz * vz);
+        return (c1 | c2 | c3) ? len : m * 0.57735027f;
+#else
         float q0, q1, q2;
         if (3.0f * ax < m) {
             q0 = ax; q1 = ay; q2 = az;
@@ -201,6 +212,7 @@ __device__ __forceinline__ float sdf_k(const PtNode &n, float x, float y, float 
         const float k = pt_gmin(pt_gmax(0.5f * (q2 - q1 + s), 0.0f), s);
         const float vy = q1 - s + k, vz = q2 - k;
         return pt_sqrt(q0 * q0 + vy * vy + vz * vz);
+#endif
     }
 }
 __device__ __forceinline__ float sdf(const PtNode &n, float x, float y, float z) {
