@@ -220,3 +220,16 @@ def test_material_table_size_and_scale_reciprocals(tmp_path):
         inv = np.float32(nodes[int(i)]["inv"])
         assert np.float32(_value(y)) == np.float32(1.0) / inv
     assert prog.n_ops > 0
+
+
+def test_radius_test_and_bounds_forms(tmp_path):
+    """The shipped codegen choices (DESIGN.md 5 history, 3.19): the radius
+    cull test joins its point bound with `&` (no exec-mask region around the
+    test), and the shade kernels' straight-line bounds() decides its slab
+    tests by the ulp margin, one select per box bit."""
+    src, _ = _baked("c3", tmp_path)
+    cuts = re.findall(r"const bool cut = pb\d+ (&&?) \(cl \* 0x1\.ff8p-1f > cK \* cK\);", src)
+    assert cuts and set(cuts) == {"&"}, set(cuts)
+    assert "uint32_t gapu = 0xffffffffu;" in src
+    assert "__ballot(!(gapu > PT_ULP_MARGIN))" in src
+    assert re.search(r"w0 \|= ray_box_ulp\(A0, ro\.x, ro\.y, ro\.z, yx, yy, yz, gapu\) \? 0x[0-9a-f]+u : 0u;", src)
