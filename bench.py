@@ -10,7 +10,12 @@ Inputs (scene tables, image) are resident in HBM before timing.
 Multi-GPU (``torchrun --nproc-per-node N``): cyclic 8x8-tile ownership, each
 rank renders its 1/N of the tiles for N*spp frames per step (weak scaling:
 fixed samples per GPU), and the step ends with the RCCL sum-reduce of the
-accumulation image onto rank 0 (bit-identical to a 1-GPU render).
+accumulation image onto rank 0 (bit-identical to a 1-GPU render).  At N > 1
+the line also carries ``c4_strong``: BASELINE config 4 (3840x2160, 256 spp,
+8 bounces, the same scene) split over the N GPUs (strong scaling: each rank
+renders all 256 frames of its 1/N of the tiles), with the reduce timed on
+its own.  ``--config c4`` makes that the headline (``scaling: strong``);
+``--config c2|c5|c1`` bench the other single-GPU configs.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md 5 for the roofline accounting.
 """
@@ -29,7 +34,6 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Msamples/sec at 1920×1080×8-bounce; achieved HBM GB/s vs gfx950 peak"
 PEAK_F32_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (vector); wave64 v_fma_f32 issues in 2 cycles on SIMD-32
-PEAK_F32_TFLOPS_SURVEY_NONPACKED = 78.6  # SURVEY.md 8(d)'s "non-packed" figure, reported beside as it asks
 PEAK_HBM_GBS = 8000.0  # spec
 
 # Algorithmic flop weights per counted event; FMA = 2,
@@ -46,14 +50,25 @@ W_CAMERA = 25
 W_ACCUM = 10
 
 
-def trace_flops(st: dict, taps: dict) -> float:
+def shade_flops(st: dict, taps: dict, n_aabb: int) -> float:
+    """The part of algorithmic_flops() done by the binned pipeline's shade
+    passes: calc_normal's six taps when they run there (`taps`: the tap share
+    of the stats run, PathTracer.tap_stats; zeros otherwise), the bounds() of
+    every continuing ray (all slab tests but the primary rays' n_aabb per
+    sample, which the gen pass or the first trace pass run) and shading +
+    Russian roulette of every hit."""
+    return (map_flops(taps) + W_NORMAL * (taps["normal_maps"] // 6)
+            + W_AABB * (st["aabb_tests"] - st["samples"] * n_aabb) + W_SHADE * st["shaded"])
+
+
+def trace_flops(st: dict, taps: dict, n_aabb: int, gen_trace: bool) -> float:
     """The part of algorithmic_flops() done by the binned pipeline's trace
-    passes: the march (and calc_normal when its taps run there): everything
-    but bounds() and shading (shade pass), the camera ray (gen) and the
-    accumulation (fold), and the map() work of the shade pass's normal taps
-    (`taps`: the tap share of the stats run, PathTracer.tap_stats)."""
-    return (algorithmic_flops(st) - W_AABB * st["aabb_tests"] - W_SHADE * st["shaded"]
-            - (W_CAMERA + W_ACCUM) * st["samples"] - map_flops(taps) - W_NORMAL * (taps["normal_maps"] // 6))
+    passes: the march (and calc_normal when its taps run there) -- all but
+    the shade passes' share, the fold's accumulation and, unless the first
+    trace pass makes its own camera rays (gen_trace), the gen pass's camera
+    rays and primary bounds()."""
+    gen = 0.0 if gen_trace else (W_CAMERA + W_AABB * n_aabb) * st["samples"]
+    return algorithmic_flops(st) - shade_flops(st, taps, n_aabb) - W_ACCUM * st["samples"] - gen
 
 
 def map_flops(st: dict) -> float:
@@ -139,10 +154,10 @@ def schedule_metrics(st_all: dict, taps: dict) -> dict:
     return out
 
 
-def profiled_traffic(config: dict):
-    """HBM bytes per launch of the hot kernel from the newest committed
-    rocprofv3 PMC summary (profiles/*_pmc.json, scripts/summarize_profile.py)
-    taken on this same workload; None if there is none."""
+def profiled(config: dict):
+    """The newest committed rocprofv3 PMC summary (profiles/*_pmc.json,
+    scripts/summarize_profile.py) taken on this same workload, as (summary,
+    path); None if there is none."""
     import glob
 
     best = None
@@ -155,16 +170,52 @@ def profiled_traffic(config: dict):
         keys = ("width", "height", "bounces", "spp_per_step")
         same_lanes = cfg.get("pipelines", 2) == config.get("pipelines", 2)  # (older summaries: the default 2)
         if all(cfg.get(k) == config.get(k) for k in keys) and cfg.get("workload") == config.get("workload") \
-                and same_lanes:
-            hb = d.get("derived", {}).get("hbm_bytes_per_launch")
-            if hb:
-                best = (hb, os.path.relpath(f, ROOT))
+                and same_lanes and d.get("derived", {}).get("hbm_bytes_per_launch"):
+            best = (d, os.path.relpath(f, ROOT))
     return best
 
 
+def hw_view(derived: dict) -> dict:
+    """The hardware counters' view of a kernel beside its algorithmic frac:
+    VALU issue (fraction of the wave64 issue rate) x lane utilisation = the
+    fraction of FP32 lane-slots that did work."""
+    keys = ("valu_issue_frac_of_peak", "valu_lane_utilization", "salu_per_valu", "wave_time_waitcnt",
+            "wave_time_wait_issue")
+    out = {k: round(derived[k], 4) for k in keys if k in derived}
+    if "valu_issue_frac_of_peak" in out and "valu_lane_utilization" in out:
+        out["valu_lane_slots_busy"] = round(derived["valu_issue_frac_of_peak"] * derived["valu_lane_utilization"], 4)
+    return out
+
+
+def cpu_info() -> dict:
+    """Host CPU of this box: model, logical CPUs, and the CPUs this process
+    may run on (a GPU box's share can be far below os.cpu_count())."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    return {"model": model, "os_cpu_count": os.cpu_count(), "affinity": affinity}
+
+
 def cpu_baseline(scene, w, h, bounces, threads: int, row_stride: int, spp: int) -> dict:
+    import tempfile
+
     from oracle import oracle as O  # test infrastructure: the CPU restatement
 
+    info = cpu_info()
+    build = "oracle/pt_oracle.c, gcc -O3 -march=native -ffp-contract=off"
+    try:  # compiled for this host (the shipped .so targets x86-64-v3)
+        O.use_library(O.build_native(tempfile.mkdtemp(prefix="pt_oracle_")))
+    except (OSError, RuntimeError, Exception) as e:  # noqa: BLE001 - report, keep the shipped build
+        build = f"oracle/libpt_oracle.so (x86-64-v3; native build failed: {type(e).__name__})"
     osc = O.OracleScene(scene.rows())
     c = O.Constants(0.0, 1, float(np.float32(w) / np.float32(h)), 1)
     s = O.Settings(0, bounces, 1.0, 1.0, 0)
@@ -175,30 +226,123 @@ def cpu_baseline(scene, w, h, bounces, threads: int, row_stride: int, spp: int) 
     rows = len(range(0, h, row_stride))
     samples = rows * w * spp
     return {"value": samples / dt / 1e6, "unit": "Msamples/sec", "cores": threads, "kind": "port",
-            "sample": f"C oracle (oracle/pt_oracle.c, -O3, {threads} threads) on every {row_stride}th row of the "
-                      f"same {w}x{h} 8-bounce c3 frame, {spp} spp ({samples} samples, {dt:.1f} s)"}
+            "cpu_model": info["model"], "os_cpu_count": info["os_cpu_count"], "cpus_available": info["affinity"],
+            "sample": f"C oracle ({build}, {threads} threads = the CPUs this process may use) on every "
+                      f"{row_stride}th row of the same {w}x{h} {bounces}-bounce frame, {spp} spp ({samples} "
+                      f"samples, {dt:.1f} s)"}
+
+
+def default_cpu_threads() -> int:
+    """Every CPU this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS where the box sets it to its CPU share."""
+    n = cpu_info()["affinity"]
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def max_over_ranks(dist, v: float, device: str) -> float:
+    if dist is None:
+        return v
+    import torch
+
+    t = torch.tensor([v], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def reduce_probe(tr, pt, barrier, dist, device: str, reps: int = 3) -> float:
+    """ms of one image reduce alone (after the render), max over ranks,
+    median of `reps`."""
+    if tr.world == 1:
+        return 0.0
+    ts = []
+    for _ in range(reps):
+        pt.sync()
+        barrier()
+        t0 = time.perf_counter()
+        tr.reduce(0)
+        pt.sync()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return max_over_ranks(dist, float(np.median(ts)), device)
+
+
+def strong_leg(local_rank, rank, world, mode, barrier, dist, device, steps: int, warmup: int) -> dict:
+    """BASELINE config 4 (3840x2160, 256 spp, 8 bounces, the 32-node scene)
+    split over the ranks' tiles: each step renders the whole image's 256
+    frames once (every rank all 256 frames of its 1/N of the tiles) and
+    reduces it onto rank 0."""
+    from compute_path_tracer_amd import _native as N
+    from compute_path_tracer_amd import scenes
+    from compute_path_tracer_amd.distributed import TileSplitRender
+    from compute_path_tracer_amd.path_tracer import PathTracer
+    from compute_path_tracer_amd.sdf_editor import CompData
+
+    scene, w, h, spp, bounces = scenes.CONFIGS["c4"]
+    pt = PathTracer(w, h, scenes.SCENES[scene]().compile(CompData()), device=local_rank,
+                    settings=N.Settings(debug=0, bounces=bounces, scale=1.0, fov=1.0, aabb=0))
+    pt.set_option("jit_wait", 1)
+    tr = TileSplitRender(pt, rank, world, float(np.float32(w) / np.float32(h)), reduce=mode, scaling="strong")
+    for _ in range(warmup):
+        tr.step(spp)
+        tr.reduce(0)
+    pt.sync()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step(spp)
+        tr.reduce(0)
+    pt.sync()
+    barrier()
+    dt = max_over_ranks(dist, time.perf_counter() - t0, device)
+    render_ms = max_over_ranks(dist, pt.last_dispatch_ms(), device)  # the last step's render on this rank's stream
+    red = reduce_probe(tr, pt, barrier, dist, device)
+    pt.close()
+    return {"metric": "Msamples/sec, BASELINE config 4 split over the GPUs",
+            "value": round(w * h * spp * steps / dt / 1e6, 3), "unit": "Msamples/sec", "scaling": "strong",
+            "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(dt * 1e3 / steps, 3),
+            "render_ms_max_rank": round(render_ms, 3), "reduce_ms": round(red, 3),
+            "config": {"workload": f"c3 {w}x{h}, {bounces} bounces, {spp} spp per step over all GPUs",
+                       "width": w, "height": h, "bounces": bounces, "spp_per_step": spp,
+                       "parallelism": f"tiles{world}", "reduce": "RCCL ncclReduce(sum) onto rank 0"
+                       if mode == "rccl" else "host sum over torch.distributed (gloo)"}}
 
 
 def main() -> None:
+    from compute_path_tracer_amd import scenes as _scenes
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--spp", type=int, default=256,
-                    help="frames per pixel per step (per GPU-share); 256 = one step is the whole C3 render")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--bounces", type=int, default=8)
-    ap.add_argument("--scene", default="c3")
+    ap.add_argument("--config", default="c3", choices=sorted(_scenes.CONFIGS),
+                    help="BASELINE config: c3 (the metric's, default), c4 (2160p split over the GPUs: strong "
+                         "scaling), c2, c5, c1")
+    ap.add_argument("--spp", type=int, default=None,
+                    help="frames per pixel per step (per GPU-share when weak); default the config's "
+                         "(c3: 256 = one step is the whole render)")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--bounces", type=int, default=None)
+    ap.add_argument("--scene", default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may use")
     ap.add_argument("--cpu-row-stride", type=int, default=1)
     ap.add_argument("--cpu-spp", type=int, default=6)
+    ap.add_argument("--c4-steps", type=int, default=2,
+                    help="N > 1: steps of the config-4 strong-scaling leg (0 skips it)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + host image reduce: rehearsal with ranks sharing one GPU")
     ap.add_argument("--validate", action="store_true",
                     help="rank 0 re-renders every frame on one GPU and checks the assembled image bit for bit")
     args = ap.parse_args()
+    cscene, cw, ch, cspp, cb = _scenes.CONFIGS[args.config]
+    scene_name = args.scene or cscene
+    width, height = args.width or cw, args.height or ch
+    bounces = cb if args.bounces is None else args.bounces
+    spp = args.spp or cspp
+    scaling = "strong" if args.config == "c4" else "weak"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -206,6 +350,7 @@ def main() -> None:
     if os.environ.get("PT_BENCH_SHARE_GPU"):  # test aid: all ranks on GPU 0 (single-GPU boxes)
         local_rank = 0
     dist = None
+    dev = "cpu"
     if world > 1:
         import torch
         import torch.distributed as dist_
@@ -214,6 +359,7 @@ def main() -> None:
         torch.cuda.set_device(local_rank)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dev = "cuda"
         else:
             dist.init_process_group("gloo")
 
@@ -224,16 +370,17 @@ def main() -> None:
 
     from compute_path_tracer_amd.distributed import TileSplitRender
 
-    ed = scenes.SCENES[args.scene]()
+    ed = scenes.SCENES[scene_name]()
     prog = ed.compile(CompData())
-    settings = N.Settings(debug=0, bounces=args.bounces, scale=1.0, fov=1.0, aabb=0)
-    pt = PathTracer(args.width, args.height, prog, device=local_rank, settings=settings)
+    settings = N.Settings(debug=0, bounces=bounces, scale=1.0, fov=1.0, aabb=0)
+    pt = PathTracer(width, height, prog, device=local_rank, settings=settings)
     # setup, untimed: install the values-baked scene kernel (jit_bake 2 tier-up;
     # an interactive caller keeps rendering on the table kernel meanwhile)
     pt.set_option("jit_wait", 1)
-    aspect = float(np.float32(args.width) / np.float32(args.height))
-    spp_step = args.spp * world  # weak scaling: each rank owns 1/world of the tiles
-    tr = TileSplitRender(pt, rank, world, aspect, reduce="rccl" if args.dist_backend == "nccl" else "host")
+    aspect = float(np.float32(width) / np.float32(height))
+    mode = "rccl" if args.dist_backend == "nccl" else "host"
+    tr = TileSplitRender(pt, rank, world, aspect, reduce=mode, scaling=scaling)
+    spp_step = spp * world if scaling == "weak" else spp  # frames per rank per step
 
     def barrier():
         if dist is not None:
@@ -246,7 +393,7 @@ def main() -> None:
                 dist.barrier()
 
     def step():
-        tr.step(args.spp)
+        tr.step(spp)
         tr.reduce(0)  # RCCL sum of the tile images onto rank 0 (no-op at world 1)
 
     # algorithmic work per step from the instrumented kernel (outside timing)
@@ -257,14 +404,16 @@ def main() -> None:
         step()
     pt.sync()
     barrier()
-    kernel_ms, trace_ms, trace_n = [], [], []
+    kernel_ms, trace_ms, trace_n, shade_ms, shade_n = [], [], [], [], []
 
     def record_times():
         kernel_ms.append(pt.last_dispatch_ms())  # whole dispatch (all pipeline kernels)
         n = int(pt.get_option("trace_launches"))
-        if n:  # binned pipeline: the trace passes, timed by events on the library stream
+        if n:  # binned pipeline: the trace / shade passes, timed by events on each pipeline's stream
             trace_ms.append(pt.get_option("trace_ms"))
             trace_n.append(n)
+            shade_ms.append(pt.get_option("shade_ms"))
+            shade_n.append(int(pt.get_option("shade_launches")))
 
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -273,58 +422,82 @@ def main() -> None:
             record_times()
     pt.sync()
     barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = max_over_ranks(dist, time.perf_counter() - t0, dev)
     if world > 1:
         # per-launch kernel time on this rank (events on the library stream)
-        tr.step(args.spp)
+        tr.step(spp)
         record_times()
+    reduce_ms = reduce_probe(tr, pt, barrier, dist, dev)
     validation = None
     if args.validate:
         img = tr.image(0)  # every frame rendered so far, assembled on rank 0
         if rank == 0:
-            ref = PathTracer(args.width, args.height, prog, device=local_rank, settings=settings)
+            ref = PathTracer(width, height, prog, device=local_rank, settings=settings)
             ref.dispatch(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), tr.frame - 1)
             want = ref.read_image()
             validation = {"frames": tr.frame - 1,
                           "bit_exact": bool(np.array_equal(img.view(np.uint32), want.view(np.uint32)))}
             ref.close()
 
-    pixels = args.width * args.height
-    samples_step = pixels * args.spp * world  # all ranks
+    pixels = width * height
+    samples_step = pixels * spp * (world if scaling == "weak" else 1)  # all ranks
     value = samples_step * args.steps / dt / 1e6
     ms_step = dt * 1e3 / args.steps
 
-    if rank != 0:
-        if dist is not None:
-            barrier()
-            dist.destroy_process_group()
-        return
+    out = None
+    if rank == 0:
+        out = report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, spp_step, world, scaling,
+                     value, ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation)
+    pt.close()
+    if world > 1 and scaling == "weak" and args.c4_steps > 0 and not args.validate:
+        leg = strong_leg(local_rank, rank, world, mode, barrier, dist, dev, args.c4_steps, 1)
+        if out is not None:
+            out["c4_strong"] = leg
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        barrier()
+        dist.destroy_process_group()
 
+
+def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, spp_step, world, scaling, value,
+           ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation) -> dict:
+    """Rank 0's JSON line."""
     d_ms = float(np.mean(kernel_ms))  # one dispatch = one step's frames of this rank
     flops_step = algorithmic_flops(st)
     rank_pixels = st["samples"] / max(1, spp_step)
     image_bytes = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per dispatch
     jit = bool(pt.get_option("jit_active"))
-    pipe = pipeline_bytes(st, rank_pixels, gen_trace=bool(pt.get_option("gen_trace")))
+    gen_trace = bool(pt.get_option("gen_trace"))
+    pipe = pipeline_bytes(st, rank_pixels, gen_trace=gen_trace)
     shade_taps = bool(pt.get_option("shade_taps")) and jit
+    n_aabb = prog.n_aabb
+    shade = None
     if trace_n:  # dominant kernel: the binned trace pass (flops of its passes / their device time)
         hot = ("pt_bin_trace_m_jit" if shade_taps else "pt_bin_trace_jit") if jit else "pt_bin_trace_kernel"
         launches = float(np.mean(trace_n))
         t_ms = float(np.mean(trace_ms))
         k_ms = t_ms / launches
-        achieved_tf = trace_flops(st, taps) / (t_ms * 1e-3) / 1e12
+        k_flops = trace_flops(st, taps, n_aabb, gen_trace)
+        achieved_tf = k_flops / (t_ms * 1e-3) / 1e12
+        s_ms, s_n = float(np.mean(shade_ms)), float(np.mean(shade_n))
+        s_flops = shade_flops(st, taps, n_aabb)
+        s_tf = s_flops / (s_ms * 1e-3) / 1e12
+        shade = {"kernel": ("pt_bin_shade_t_jit" if shade_taps else "pt_bin_shade_kernel"),
+                 "achieved": round(s_tf, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                 "frac": round(s_tf / PEAK_F32_TFLOPS, 4), "flops_per_step": round(s_flops),
+                 "flops_per_launch": round(s_flops / max(1.0, s_n)), "ms_per_launch": round(s_ms / max(1.0, s_n), 3),
+                 "launches_per_step": s_n, "ms_per_step_summed": round(s_ms, 3),
+                 "scope": "calc_normal's six taps (map() work + 29), bounds() of continuing rays (40 per slab test) "
+                          "and shading + RR (100 per hit) / the shade launches' HIP-event time"}
     else:  # the tile-resident kernels do the whole path in one launch
         hot = "pt_wave_jit" if jit else "pt_wave_kernel"
         launches, t_ms, k_ms = 1.0, d_ms, d_ms
+        k_flops = flops_step
         achieved_tf = flops_step / (d_ms * 1e-3) / 1e12
     path_tf = flops_step / (d_ms * 1e-3) / 1e12
     achieved_gbs = pipe["total"] / (d_ms * 1e-3) / 1e9  # whole dispatch: every pass's algorithmic bytes
+    data = f"synthetic (scenes.{scenes_fn(scene_name)}"
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -334,15 +507,16 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (scenes.c3_graph32: 32-node sdf_editor graph, seed 42)",
-        "config": {"workload": f"{args.scene} {args.width}x{args.height}, {args.bounces} bounces, "
-                               f"{args.spp * world} spp per step ({args.spp} per GPU-share), progressive accumulate",
-                   "width": args.width, "height": args.height, "bounces": args.bounces,
-                   "spp_per_step": args.spp * world, "parallelism": f"tiles{world}",
-                   "pipelines": int(pt.get_option("bin_lanes"))},
+        "data": data + ("" if scene_name != "c3" else ": 32-node sdf_editor graph, seed 42") + ")",
+        "config": {"workload": f"{scene_name} {width}x{height}, {bounces} bounces, "
+                               + (f"{spp * world} spp per step ({spp} per GPU-share)" if scaling == "weak"
+                                  else f"{spp} spp per step over all GPUs") + ", progressive accumulate",
+                   "width": width, "height": height, "bounces": bounces,
+                   "spp_per_step": spp * world if scaling == "weak" else spp, "parallelism": f"tiles{world}",
+                   "pipelines": int(pt.get_option("bin_lanes")), "baseline_config": args.config},
         "roofline": {"bound": "valu",
                      "bound_note": "FP32 vector ALU: no dense contraction on this path, so no MFMA, and arithmetic "
                                    "intensity ~65 flop/B of measured traffic is above the HBM ridge; the metric's "
@@ -351,15 +525,17 @@ def main() -> None:
                      "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_TFLOPS, 4), "traffic": None,
                      "traffic_source": None,
                      "algorithmic_flops_per_sample": round(flops_step / max(1, st["samples"]), 1),
-                     "kernel_flops_per_launch": round((trace_flops(st, taps) if trace_n else flops_step) / launches),
-                     "shade_tap_flops_per_step": round(map_flops(taps) + W_NORMAL * (taps["normal_maps"] // 6)),
-                     "frac_vs_78_6": round(achieved_tf / PEAK_F32_TFLOPS_SURVEY_NONPACKED, 4),
+                     "kernel_flops_per_launch": round(k_flops / launches),
+                     "kernel_scope": "trace passes (the first with its camera rays and primary bounds()) : march "
+                                     "map() work + 10 per step" if gen_trace else "trace passes: march",
                      "kernel_ms_per_launch": round(k_ms, 3), "kernel_launches_per_step": launches,
                      "dispatch_ms_per_step": round(d_ms, 3),
                      "path_achieved": round(path_tf, 3), "path_frac": round(path_tf / PEAK_F32_TFLOPS, 4)},
         "hbm": {"achieved": round(achieved_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved_gbs / PEAK_HBM_GBS, 6),
-                "scope": "binned pipeline's algorithmic bytes per dispatch (all passes) / dispatch time",
+                "scope": "the binned pipeline's own algorithmic bytes per dispatch (all passes: 64 B ray records "
+                         "between passes, the price of binning) / dispatch time; SURVEY 8(d)'s algorithmic bytes "
+                         "of the metric are the image's 32 B per pixel per dispatch (image_gbs)",
                 "algorithmic_bytes_per_dispatch": pipe["total"],
                 "bytes_per_sample": round(pipe["total"] / max(1, st["samples"]), 1),
                 "by_pass": {k: v for k, v in pipe.items() if k != "total"},
@@ -371,29 +547,42 @@ def main() -> None:
                 "tier_active": bool(pt.get_option("jit_tier_active")),
                 "tier_compile_s": round(pt.get_option("jit_tier_seconds"), 3)},
     }
+    if shade is not None:
+        out["roofline"]["shade"] = shade
+    if world > 1:
+        out["reduce_ms"] = round(reduce_ms, 3)
     if validation is not None:
         out["validation"] = validation
     # display pass, outside the timed region: HBM-bound
     # elementwise kernel, 16 B read + 4 B written per pixel (sRGB8 surface)
     pt.display(srgb8=True)
     dms = [pt.get_option("display_ms") for _ in range(3) if pt.display(srgb8=True) is not None]
-    d_ms = float(min(dms))
-    d_bytes = 20.0 * args.width * args.height
-    out["display"] = {"kernel": "pt_display_kernel (srgb8)", "ms": round(d_ms, 4),
-                      "achieved_gbs": round(d_bytes / (d_ms * 1e-3) / 1e9, 1), "peak_gbs": PEAK_HBM_GBS,
+    disp_ms = float(min(dms))
+    d_bytes = 20.0 * width * height
+    out["display"] = {"kernel": "pt_display_kernel (srgb8)", "ms": round(disp_ms, 4),
+                      "achieved_gbs": round(d_bytes / (disp_ms * 1e-3) / 1e9, 1), "peak_gbs": PEAK_HBM_GBS,
                       "algorithmic_bytes": d_bytes}
-    tr_prof = profiled_traffic(out["config"])
-    if tr_prof is not None:
-        out["roofline"]["traffic"] = tr_prof[0]
-        out["roofline"]["traffic_source"] = f"{tr_prof[1]} (2*FETCH_SIZE+WRITE_SIZE, KiB->B, per launch)"
-        out["hbm"]["trace_kernel_measured_bytes_per_launch"] = tr_prof[0]
+    prof = profiled(out["config"])
+    if prof is not None:
+        pd, src = prof
+        hb = pd["derived"]["hbm_bytes_per_launch"]
+        out["roofline"]["traffic"] = hb
+        out["roofline"]["traffic_source"] = f"{src} (2*FETCH_SIZE+WRITE_SIZE, KiB->B, per launch)"
+        out["hbm"]["trace_kernel_measured_bytes_per_launch"] = hb
+        out["roofline"]["hw"] = dict(hw_view(pd["derived"]), source=src)
+        sk = (pd.get("other_kernels") or {}).get(shade["kernel"]) if shade else None
+        if sk:
+            out["roofline"]["shade"]["hw"] = dict(hw_view(sk), source=src)
     if not args.no_cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(ed, args.width, args.height, args.bounces, args.cpu_threads,
-                                           args.cpu_row_stride, args.cpu_spp)
-    print(json.dumps(out), flush=True)
-    if dist is not None:
-        barrier()
-        dist.destroy_process_group()
+        threads = args.cpu_threads or default_cpu_threads()
+        out["cpu_baseline"] = cpu_baseline(ed, width, height, bounces, threads, args.cpu_row_stride, args.cpu_spp)
+    return out
+
+
+def scenes_fn(name: str) -> str:
+    from compute_path_tracer_amd import scenes
+
+    return scenes.SCENES[name].__name__
 
 
 if __name__ == "__main__":

@@ -47,6 +47,7 @@ SYMBOLS = (
     "pt_dispatch_stats", "pt_set_option", "pt_get_option", "pt_jit_log", "pt_jit_compile", "pt_last_error",
     "pt_destroy", "pt_abi_version", "pt_device_math", "pt_check_sqrt_exhaustive", "pt_check_div_exhaustive",
     "pt_check_div_random", "pt_check_box_random", "pt_check_div_k", "pt_display", "pt_write_accum",
+    "pt_compile_scene_keyed", "pt_save_rgba8",
 )
 PT_MATH = {"max": 0, "min": 1, "sqrt": 2, "sqrtf": 3, "sin": 4, "cos": 5, "div": 6, "fma": 7}
 
@@ -69,6 +70,15 @@ class SceneNode(Structure):
         ("scale", c_float), ("position", c_float * 3), ("rotation", c_float * 3), ("aabb_exaggeration", c_float),
         ("size", c_float * 3), ("material", c_float * 18),
     ]
+
+
+PT_NODE_FLOATS = 29
+
+
+class FloatKey(Structure):
+    """pt_float_key: a Float's u128 serde hash (lo, hi); {0, 0} = anonymous."""
+
+    _fields_ = [("lo", c_uint64), ("hi", c_uint64)]
 
 
 class Op(Structure):
@@ -114,6 +124,9 @@ def lib() -> ctypes.CDLL:
     sig = {
         "pt_compile_scene": (c_int, [POINTER(SceneNode), c_uint32, POINTER(Op), c_uint32, u32p, POINTER(Aabb), c_uint32,
                                      u32p, POINTER(c_float), c_uint32, u32p, u32p]),
+        "pt_compile_scene_keyed": (c_int, [POINTER(SceneNode), c_uint32, POINTER(FloatKey), POINTER(Op), c_uint32, u32p,
+                                           POINTER(Aabb), c_uint32, u32p, POINTER(c_float), c_uint32, u32p, u32p]),
+        "pt_save_rgba8": (c_int, [POINTER(c_float), c_uint32, c_uint32, POINTER(c_uint8), c_size_t]),
         "pt_create": (c_int, [c_int, c_uint32, c_uint32, POINTER(ctx)]),
         "pt_resize_clear": (c_int, [ctx, c_uint32, c_uint32]),
         "pt_set_program": (c_int, [ctx, POINTER(Op), c_uint32, POINTER(Aabb), c_uint32, c_uint32]),

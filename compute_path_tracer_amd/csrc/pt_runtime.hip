@@ -104,8 +104,12 @@ struct pt_ctx {
     bool fast_bounds = false;  // every box coordinate inside the reciprocal-division guard
     float bound_k = 0.0f;      // pt_bound_k of the uploaded scene (NaN: no map() bound)
     // HIP events around each trace-pass launch of the last dispatch (pairs)
-    std::vector<hipEvent_t> tev;
-    size_t tev_used = 0;
+    // HIP event pairs around the last dispatch's binned trace / shade launches
+    // (on each pipeline's stream): their summed device time per kernel
+    struct EventLog {
+        std::vector<hipEvent_t> ev;
+        size_t used = 0;
+    } tlog, slog;
     // display pass output (device) and its timing
     void *d_display = nullptr;
     size_t cap_display = 0;
@@ -620,8 +624,13 @@ int pt_set_tiles(pt_ctx *c, uint32_t rank, uint32_t nranks) {
 // per sample of a chunk: two ray buffers, bin key, binned slot, colour (+ the
 // high mask words and hit records' high check[] words of scenes with > 64 entries)
 constexpr size_t kBinBytesPerSample = 2 * sizeof(PtRay) + 2 * sizeof(uint32_t) + sizeof(float4);
+constexpr size_t kBinBytesWide = sizeof(uint2) + sizeof(float4);
 
-static size_t bin_samples(const pt_ctx *c) {
+static size_t bin_bytes_per_sample(const pt_ctx *c) {
+    return kBinBytesPerSample + (c->n_check > 64 ? kBinBytesWide : 0);
+}
+
+static size_t bin_samples(pt_ctx *c) {
     if (c->bin_samples > 0) return size_t(c->bin_samples);
     static const long env = [] {
         const char *v = std::getenv("PT_BIN_SAMPLES");
@@ -631,12 +640,15 @@ static size_t bin_samples(const pt_ctx *c) {
     // default: 2^29 samples (a whole 256-spp 1080p render: 82 GB of HBM at
     // 152 B per sample; every pass's tail is paid once per chunk, so larger
     // chunks are faster: 64 -> 256 frames per chunk +5 %), at most half of
-    // the device's memory
-    static const size_t cap = [] {
-        size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || total_b == 0) return size_t(1) << 27;
-        return std::max<size_t>(size_t(1) << 20, total_b / 2 / kBinBytesPerSample);
-    }();
+    // what this context could hold on its device: the free memory plus the
+    // chunk buffers it already owns (other contexts' allocations count as
+    // used, so several ranks sharing one GPU each size to what is left)
+    const size_t per = bin_bytes_per_sample(c);
+    size_t free_b = 0, total_b = 0;
+    if (hipSetDevice(c->device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess || total_b == 0)
+        return size_t(1) << 27;
+    const size_t held = c->bin_cap * size_t(c->n_lanes) * per;
+    const size_t cap = std::max<size_t>(size_t(1) << 20, (free_b + held) / 2 / per);
     return std::min<size_t>(size_t(1) << 29, cap);
 }
 
@@ -728,14 +740,27 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
     return PT_OK;
 }
 
-static hipError_t record_trace_event(pt_ctx *c, hipStream_t stream) {
-    if (c->tev_used == c->tev.size()) {
+static hipError_t record_event(pt_ctx::EventLog &g, hipStream_t stream) {
+    if (g.used == g.ev.size()) {
         hipEvent_t e;
         const hipError_t err = hipEventCreate(&e);
         if (err != hipSuccess) return err;
-        c->tev.push_back(e);
+        g.ev.push_back(e);
     }
-    return hipEventRecord(c->tev[c->tev_used++], stream);
+    return hipEventRecord(g.ev[g.used++], stream);
+}
+
+// Summed elapsed time of the log's (start, end) pairs; blocks for the last.
+static hipError_t event_log_ms(pt_ctx::EventLog &g, double *sum) {
+    *sum = 0.0;
+    if (!g.used) return hipSuccess;
+    hipError_t e = hipEventSynchronize(g.ev[g.used - 1]);
+    for (size_t i = 0; e == hipSuccess && i + 1 < g.used; i += 2) {
+        float ms = 0.0f;
+        e = hipEventElapsedTime(&ms, g.ev[i], g.ev[i + 1]);
+        *sum += ms;
+    }
+    return e;
 }
 
 // One dispatch chunk through the pass pipeline: frames are processed in
@@ -865,8 +890,11 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         const bool full_tiles = L.width % PT_TILE == 0 && L.height % PT_TILE == 0 && L.debug == 0;
         for (int i = 0; i < nl && !gen_bin && full_tiles; ++i) {
             P[i].gen_order = 1;
-            const uint32_t ctrl0[2] = {P[i].n_src_const, 0u};
-            HIPCHK(c, hipMemcpyAsync(c->lane[i].ctrl, ctrl0, sizeof ctrl0, hipMemcpyHostToDevice, c->lane[i].stream));
+            // ctrl words 0-1 = {count, 0}: stream-ordered fills, no host
+            // buffer whose lifetime the copy would have to outlast
+            HIPCHK(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->lane[i].ctrl), int(P[i].n_src_const), 1,
+                                        c->lane[i].stream));
+            HIPCHK(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->lane[i].ctrl + 1), 0, 1, c->lane[i].stream));
         }
         static const int gen_jit = [] {  // A/B knob: PT_GEN_JIT=0 keeps the ahead-of-time gen kernel
             const char *v = std::getenv("PT_GEN_JIT");
@@ -899,6 +927,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             S.bounce = k;
             S.rin = c->lane[i].ray[(k + 1) & 1];
             S.n_src = c->lane[i].ctrl + 4 * k;
+            if (!stats) HIPCHK(c, record_event(c->slog, c->lane[i].stream));
             if (taps_shade) {
                 void *args[] = {&S};
                 HIPCHK(c, hipModuleLaunchKernel(stats ? jm->shade_t_stats : jm->shade_t, shade_grid, 1, 1, PT_BIN_BLOCK,
@@ -907,6 +936,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 pt_launch_bin(PtBinStage::Shade, S, stats, shade_grid, c->lane[i].stream);
                 HIPCHK(c, hipGetLastError());
             }
+            if (!stats) HIPCHK(c, record_event(c->slog, c->lane[i].stream));
             return PT_OK;
         };
         for (int k = 0; k < passes; ++k) {
@@ -928,7 +958,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                                   l.stream);
                     HIPCHK(c, hipGetLastError());
                 }
-                if (!stats) HIPCHK(c, record_trace_event(c, l.stream));
+                if (!stats) HIPCHK(c, record_event(c->tlog, l.stream));
                 if (jit) {
                     void *args[] = {&p};
                     HIPCHK(c, hipModuleLaunchKernel(gt ? jm->trace_g : jf, trace_grid, 1, 1, 64, 1, 1, 0, l.stream, args,
@@ -937,7 +967,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                     pt_launch_bin(PtBinStage::Trace, p, stats, trace_grid, l.stream);
                     HIPCHK(c, hipGetLastError());
                 }
-                if (!stats) HIPCHK(c, record_trace_event(c, l.stream));
+                if (!stats) HIPCHK(c, record_event(c->tlog, l.stream));
             }
         }
         for (int i = 0; i < nl; ++i)  // the last bounce's hits end their paths
@@ -1038,7 +1068,7 @@ int pt_dispatch(pt_ctx *c, const pt_constants *k, const pt_settings *s, uint32_t
     HIPCHK(c, hipSetDevice(c->device));
     jit_tier_poll(c, false);  // switch to the values-baked kernel once it is built
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    c->tev_used = 0;
+    c->tlog.used = c->slog.used = 0;
     if (spp > 0 && L.n_tiles > 0) {
         // bound a single launch's length; chunks continue frame/last_clear.
         // The binned pipeline takes every frame at once: it splits by its own
@@ -1258,23 +1288,16 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "kernel")) *value = c->kernel;
     else if (!std::strcmp(key, "shade_batch")) *value = c->shade_batch;
     else if (!std::strcmp(key, "bin_samples")) *value = double(bin_samples(c));
-    else if (!std::strcmp(key, "trace_launches")) *value = double(c->tev_used / 2);
+    else if (!std::strcmp(key, "trace_launches")) *value = double(c->tlog.used / 2);
+    else if (!std::strcmp(key, "shade_launches")) *value = double(c->slog.used / 2);
     else if (!std::strcmp(key, "display_ms")) {
         float ms = 0.0f;
         if (c->display_timed) HIPCHK(c, hipEventElapsedTime(&ms, c->dev0, c->dev1));
         *value = ms;
     }
-    else if (!std::strcmp(key, "trace_ms")) {  // summed device time of the last dispatch's trace passes
-        double sum = 0.0;
-        if (c->tev_used) HIPCHK(c, hipEventSynchronize(c->tev[c->tev_used - 1]));
-        for (size_t i = 0; i + 1 < c->tev_used; i += 2) {
-            float ms = 0.0f;
-            HIPCHK(c, hipEventElapsedTime(&ms, c->tev[i], c->tev[i + 1]));
-            sum += ms;
-        }
-        *value = sum;
-    }
-    else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * double(c->n_lanes) * kBinBytesPerSample;
+    else if (!std::strcmp(key, "trace_ms")) HIPCHK(c, event_log_ms(c->tlog, value));  // summed over the trace passes
+    else if (!std::strcmp(key, "shade_ms")) HIPCHK(c, event_log_ms(c->slog, value));  // summed over the shade passes
+    else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * double(c->n_lanes) * double(bin_bytes_per_sample(c));
     else if (!std::strcmp(key, "bin_lanes")) *value = double(bin_lanes(c));
     else if (!std::strcmp(key, "shade_taps")) *value = shade_taps(c) ? 1.0 : 0.0;
     else if (!std::strcmp(key, "gen_trace")) *value = double(c->gen_trace_used);
@@ -1313,7 +1336,8 @@ void pt_destroy(pt_ctx *c) {
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->tlog.ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->slog.ev) (void)hipEventDestroy(e);
     (void)hipFree(c->d_display);
     if (c->dev0) (void)hipEventDestroy(c->dev0);
     if (c->dev1) (void)hipEventDestroy(c->dev1);

@@ -14,6 +14,8 @@
 // pins it against the captured compiler output), so a Rust host keeps its
 // CompData/DataArray unchanged.  Host code only.
 #include <cstring>
+#include <map>
+#include <utility>
 #include <vector>
 
 #include "../../include/pt_abi.h"
@@ -27,12 +29,28 @@ struct Tree {
     std::vector<uint32_t> top;
 };
 
+// Float positions inside a node's key block (pt_abi.h PT_NODE_FLOATS)
+enum { KF_SCALE = 0, KF_POS = 1, KF_ROT = 4, KF_EX = 7, KF_SIZE = 8, KF_MAT = 11 };
+
 struct Emit {
     std::vector<float> data;
     std::vector<pt_op> ops;
     std::vector<pt_aabb> aabbs;
     uint32_t aabb_index = 0;
-    uint32_t slot(float v) {  // DataArray::get_index: every Float has its own hash -> fresh slot
+    const pt_float_key *keys = nullptr;  // [node][PT_NODE_FLOATS], or none
+    std::map<std::pair<uint64_t, uint64_t>, uint32_t> seen;
+    // DataArray::get_index (primitives.rs:117-129): a Float whose hash was
+    // seen before reuses that slot (its value stays the first one's); a new
+    // hash -- or an anonymous Float, key {0, 0} -- appends a slot
+    uint32_t slot(float v, uint32_t node, uint32_t k) {
+        if (keys) {
+            const pt_float_key &key = keys[size_t(node) * PT_NODE_FLOATS + k];
+            if (key.lo | key.hi) {
+                auto it = seen.find({key.lo, key.hi});
+                if (it != seen.end()) return it->second;
+                seen.emplace(std::make_pair(key.lo, key.hi), uint32_t(data.size()));
+            }
+        }
         data.push_back(v);
         return uint32_t(data.size() - 1);
     }
@@ -52,13 +70,14 @@ uint32_t size_count(int32_t kind) {
     }
 }
 
-// Transform::compile: scale, position.xyz, scale (reused), rotation.xyz, aabb_exaggeration
-Slots transform(Emit &e, const pt_scene_node &n) {
+// Transform::compile (data_structures.rs:45-55): scale, position.xyz, scale
+// again (get_index of a seen hash: no new slot), rotation.xyz, aabb_exaggeration
+Slots transform(Emit &e, const pt_scene_node &n, uint32_t node) {
     Slots s;
-    s.scale = e.slot(n.scale);
-    for (int i = 0; i < 3; ++i) s.pos[i] = e.slot(n.position[i]);
-    for (int i = 0; i < 3; ++i) s.rot[i] = e.slot(n.rotation[i]);
-    s.ex = e.slot(n.aabb_exaggeration);
+    s.scale = e.slot(n.scale, node, KF_SCALE);
+    for (uint32_t i = 0; i < 3; ++i) s.pos[i] = e.slot(n.position[i], node, KF_POS + i);
+    for (uint32_t i = 0; i < 3; ++i) s.rot[i] = e.slot(n.rotation[i], node, KF_ROT + i);
+    s.ex = e.slot(n.aabb_exaggeration, node, KF_EX);
     return s;
 }
 
@@ -85,7 +104,7 @@ void compile_union(const Tree &t, Emit &e, uint32_t u, int32_t type_in, std::vec
     std::memset(&begin, 0, sizeof begin);
     begin.opcode = PT_OP_UNION_BEGIN;
     begin.check = -1;
-    Slots us = transform(e, un);
+    Slots us = transform(e, un, u);
     slots_of[u] = us;
     fill(begin, us);
     e.ops.push_back(begin);
@@ -97,13 +116,13 @@ void compile_union(const Tree &t, Emit &e, uint32_t u, int32_t type_in, std::vec
         std::memset(&op, 0, sizeof op);
         op.opcode = PT_OP_SHAPE;
         op.shape = uint32_t(sn.kind);
-        Slots ss = transform(e, sn);
+        Slots ss = transform(e, sn, c);
         slots_of[c] = ss;
         fill(op, ss);
         uint32_t nsz = size_count(sn.kind);
-        for (uint32_t k = 0; k < nsz; ++k) op.size[k] = e.slot(sn.size[k]);
+        for (uint32_t k = 0; k < nsz; ++k) op.size[k] = e.slot(sn.size[k], c, KF_SIZE + k);
         for (uint32_t k = nsz; k < 3; ++k) op.size[k] = op.size[nsz ? nsz - 1 : 0];
-        for (int k = 0; k < 18; ++k) op.material[k] = e.slot(sn.material[k]);
+        for (uint32_t k = 0; k < 18; ++k) op.material[k] = e.slot(sn.material[k], c, KF_MAT + k);
         // Transform::aabb_check: the index advances for every shape, aabb or not
         op.check = sn.aabb ? int32_t(e.aabb_index) : -1;
         e.aabb_index++;
@@ -119,9 +138,10 @@ void compile_union(const Tree &t, Emit &e, uint32_t u, int32_t type_in, std::vec
 
 }  // namespace
 
-extern "C" int pt_compile_scene(const pt_scene_node *nodes, uint32_t n_nodes, pt_op *ops, uint32_t ops_cap,
-                                uint32_t *n_ops, pt_aabb *aabbs, uint32_t aabb_cap, uint32_t *n_aabb, float *data,
-                                uint32_t data_cap, uint32_t *n_data, uint32_t *n_check) {
+extern "C" int pt_compile_scene_keyed(const pt_scene_node *nodes, uint32_t n_nodes, const pt_float_key *keys,
+                                      pt_op *ops, uint32_t ops_cap, uint32_t *n_ops, pt_aabb *aabbs, uint32_t aabb_cap,
+                                      uint32_t *n_aabb, float *data, uint32_t data_cap, uint32_t *n_data,
+                                      uint32_t *n_check) {
     if (n_nodes > 0 && !nodes) return PT_ERR_INVALID;
     Tree t;
     t.n = nodes;
@@ -149,6 +169,7 @@ extern "C" int pt_compile_scene(const pt_scene_node *nodes, uint32_t n_nodes, pt
     if (plane) return PT_ERR_UNSUPPORTED;  // Shapes::Plane emits NotImplemented(...) upstream
 
     Emit e;
+    e.keys = keys;
     e.data.push_back(6969.69f);  // CompData::reset_data_array (primitives.rs:53-56)
     std::vector<Slots> slots_of(n_nodes);
     std::vector<size_t> op_of(n_nodes, 0);
@@ -205,4 +226,11 @@ extern "C" int pt_compile_scene(const pt_scene_node *nodes, uint32_t n_nodes, pt
         else std::memcpy(data, e.data.data(), e.data.size() * sizeof(float));
     }
     return small ? PT_ERR_SIZE : PT_OK;
+}
+
+extern "C" int pt_compile_scene(const pt_scene_node *nodes, uint32_t n_nodes, pt_op *ops, uint32_t ops_cap,
+                                uint32_t *n_ops, pt_aabb *aabbs, uint32_t aabb_cap, uint32_t *n_aabb, float *data,
+                                uint32_t data_cap, uint32_t *n_data, uint32_t *n_check) {
+    return pt_compile_scene_keyed(nodes, n_nodes, nullptr, ops, ops_cap, n_ops, aabbs, aabb_cap, n_aabb, data, data_cap,
+                                  n_data, n_check);
 }

@@ -39,17 +39,24 @@ def torch_broadcast_object(obj, src: int = 0):
 class TileSplitRender:
     """Progressive render of one image across ``world`` ranks.
 
-    Weak scaling in samples: a step of ``spp`` frames per GPU-share renders
-    ``spp * world`` frames of this rank's 1/world of the tiles, i.e. the same
-    per-GPU work at any world size; frames keep the reference's counters
-    (frame j = frame0 + j, last_clear j = last_clear0 + j, path_tracer.rs:110-111).
+    scaling="weak" (the default): a step of ``spp`` frames per GPU-share
+    renders ``spp * world`` frames of this rank's 1/world of the tiles, i.e.
+    the same per-GPU work at any world size.  scaling="strong" (BASELINE
+    config 4: one 256-spp image split over the GPUs): a step renders ``spp``
+    frames of this rank's tiles, the whole image's work divided by world.
+    Frames keep the reference's counters (frame j = frame0 + j, last_clear
+    j = last_clear0 + j, path_tracer.rs:110-111).
     """
 
     def __init__(self, renderer, rank: int, world: int, aspect: float,
-                 broadcast: Optional[Callable] = None, frame0: int = 1, reduce: str = "rccl"):
+                 broadcast: Optional[Callable] = None, frame0: int = 1, reduce: str = "rccl",
+                 scaling: str = "weak"):
         """reduce="rccl": pt_reduce_accum inside the library (RCCL over xGMI).
         reduce="host": copy to host and sum with torch.distributed (gloo) --
         a rehearsal aid for ranks that share one GPU, where RCCL refuses."""
+        if scaling not in ("weak", "strong"):
+            raise ValueError(f"scaling must be weak or strong, got {scaling!r}")
+        self.scaling = scaling
         self.r = renderer
         self.rank, self.world = rank, world
         self.aspect = float(aspect)
@@ -67,8 +74,9 @@ class TileSplitRender:
         return N.Constants(time=0.0, frame=self.frame, aspect=self.aspect, last_clear=self.last_clear)
 
     def step(self, spp_per_share: int) -> int:
-        """Render ``spp_per_share * world`` frames of this rank's tiles."""
-        n = spp_per_share * self.world
+        """Render ``spp_per_share * world`` (weak) or ``spp_per_share``
+        (strong) frames of this rank's tiles."""
+        n = spp_per_share * self.world if self.scaling == "weak" else spp_per_share
         self.r.dispatch(self.constants(), n)
         self.frame += n
         self.last_clear += n

@@ -205,6 +205,11 @@ class PathTracer:
     def reduce(self, root: int = 0) -> None:
         self._chk("pt_reduce_accum", self._L.pt_reduce_accum(self._ctx, root))
 
+    def save_image(self) -> np.ndarray:
+        """State::save_image (state.rs:237-303) without the PNG encoder: the
+        blocking readback plus the 8-bit gamma transform (row 0 = top)."""
+        return save_image_rgba8(self.read_image())
+
     def read_reduced(self) -> np.ndarray:
         w, h = self.size
         out = np.empty((h, w, 4), dtype=np.float32)
@@ -214,15 +219,18 @@ class PathTracer:
 
 
 def save_image_rgba8(img: np.ndarray) -> np.ndarray:
-    """State::save_image pixel transform (state.rs:277-289): powf(1/2.2) * 255
-    as u8 (saturating, NaN -> 0), alpha * 255, rows flipped (row 0 = top)."""
-    v = img.astype(np.float32)
-    rgb = np.power(v[..., :3], np.float32(1.0 / 2.2)) * np.float32(255.0)
-    a = v[..., 3:4] * np.float32(255.0)
-    out = np.concatenate([rgb, a], axis=-1)
-    out = np.nan_to_num(out, nan=0.0, posinf=255.0, neginf=0.0)
-    out = np.clip(np.trunc(out), 0, 255).astype(np.uint8)
-    return out[::-1].copy()
+    """State::save_image pixel transform (state.rs:277-289) on the host, in
+    the library (pt_save_rgba8): (v.powf(1.0 / 2.2) * 255.0) as u8 with
+    Rust's f32 1.0 / 2.2 and libm powf, alpha * 255, `as u8` saturating (NaN
+    -> 0), rows flipped (row 0 = top)."""
+    a = np.ascontiguousarray(img, np.float32)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise ValueError(f"image must be (h, w, 4), got {a.shape}")
+    h, w = a.shape[:2]
+    out = np.empty((h, w, 4), np.uint8)
+    N.check("pt_save_rgba8", N.lib().pt_save_rgba8(a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), w, h,
+                                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), out.nbytes))
+    return out
 
 
 def save_png(img: np.ndarray, path: str) -> None:

@@ -143,6 +143,12 @@ class Transform:
         for f in self.floats():
             f.rehash()
 
+    def refresh(self, comp_data):
+        """data_structures.rs:98-103 (position, rotation, scale, exaggeration:
+        with shared hashes the last write wins, so the order matters)."""
+        for f in (*self.position.floats(), *self.rotation.floats(), self.scale, self.aabb_exaggeration):
+            f.refresh(comp_data)
+
     def to_json(self):
         return {"position": self.position.to_json(), "rotation": self.rotation.to_json(),
                 "scale": self.scale.to_json(), "aabb_exaggeration": self.aabb_exaggeration.to_json(),
@@ -271,7 +277,9 @@ class Shape:
         self.transform.rehash(); self.material.rehash(); self.current_shape.rehash()
 
     def refresh(self, comp_data):
-        for f in self.floats():
+        """containers.rs:466-470: transform, material, then the shape's size."""
+        self.transform.refresh(comp_data)
+        for f in (*self.material.floats(), *self.current_shape.floats()):
             f.refresh(comp_data)
 
     def to_json(self):
@@ -304,8 +312,8 @@ class Union:
         self.children_shapes: List[Shape] = []
 
     def refresh(self, comp_data):
-        for f in self.transform.floats():
-            f.refresh(comp_data)
+        """containers.rs:204-212: transform, shapes, then child unions."""
+        self.transform.refresh(comp_data)
         for s in self.children_shapes:
             s.refresh(comp_data)
         for u in self.children_unions:
@@ -414,6 +422,28 @@ class Program:
         return out
 
 
+def node_keys(t: Transform, size: List[Float], material: Optional[Material]) -> List[int]:
+    """The node's Float hashes in pt_float_key order (PT_NODE_FLOATS): scale,
+    position xyz, rotation xyz, exaggeration, size[3], material[18]; 0 where
+    the node has no such Float."""
+    keys = [f.hash for f in t.floats()]
+    keys += [f.hash for f in size] + [0] * (3 - len(size))
+    keys += [f.hash for f in material.floats()] if material is not None else [0] * 18
+    return keys
+
+
+def keys_to_ctypes(rows: List[dict]):
+    """Rows' "keys" as a pt_float_key array (None when no row carries keys)."""
+    if not any(r.get("keys") for r in rows):
+        return None
+    arr = (N.FloatKey * (max(1, len(rows)) * N.PT_NODE_FLOATS))()
+    for i, r in enumerate(rows):
+        for k, h in enumerate(r.get("keys") or []):
+            arr[i * N.PT_NODE_FLOATS + k].lo = h & 0xFFFFFFFFFFFFFFFF
+            arr[i * N.PT_NODE_FLOATS + k].hi = (h >> 64) & 0xFFFFFFFFFFFFFFFF
+    return arr
+
+
 def flatten(header_unions: List[Union]) -> Tuple[List[dict], List[object]]:
     """Pre-order flattening: each node's parent precedes it; a union's child
     unions precede its shapes (the order Union::compile visits them)."""
@@ -428,7 +458,7 @@ def flatten(header_unions: List[Union]) -> Tuple[List[dict], List[object]]:
                      else N.PT_UNION_TYPE_UNION, "aabb": int(t.aabb), "scale": t.scale.val,
                      "position": t.position.vals(), "rotation": t.rotation.vals(),
                      "aabb_exaggeration": t.aabb_exaggeration.val, "size": [0.0, 0.0, 0.0],
-                     "material": [0.0] * 18})
+                     "material": [0.0] * 18, "keys": node_keys(t, [], None)})
         objs.append(u)
         for c in u.children_unions:
             visit(c, idx)
@@ -438,7 +468,8 @@ def flatten(header_unions: List[Union]) -> Tuple[List[dict], List[object]]:
             rows.append({"kind": Shapes.KIND[s.current_shape.kind], "parent": idx, "union_type": 0,
                          "aabb": int(st.aabb), "scale": st.scale.val, "position": st.position.vals(),
                          "rotation": st.rotation.vals(), "aabb_exaggeration": st.aabb_exaggeration.val,
-                         "size": sz, "material": s.material.values()})
+                         "size": sz, "material": s.material.values(),
+                         "keys": node_keys(st, s.current_shape.params, s.material)})
             objs.append(s)
 
     for u in header_unions:
@@ -463,20 +494,22 @@ def nodes_to_ctypes(rows: List[dict]) -> ctypes.Array:
 
 
 def compile_rows(rows: List[dict]) -> Program:
-    """Native pt_compile_scene on flattened rows (two-call pattern)."""
+    """Native pt_compile_scene_keyed on flattened rows (two-call pattern):
+    Floats sharing a hash share a data[] slot (DataArray::get_index)."""
     L = N.lib()
     nodes = nodes_to_ctypes(rows)
+    keys = keys_to_ctypes(rows)
     n_ops, n_aabb, n_data, n_check = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
-    rc = L.pt_compile_scene(nodes, len(rows), None, 0, ctypes.byref(n_ops), None, 0, ctypes.byref(n_aabb), None, 0,
-                            ctypes.byref(n_data), ctypes.byref(n_check))
-    N.check("pt_compile_scene", rc)
+    rc = L.pt_compile_scene_keyed(nodes, len(rows), keys, None, 0, ctypes.byref(n_ops), None, 0, ctypes.byref(n_aabb),
+                                  None, 0, ctypes.byref(n_data), ctypes.byref(n_check))
+    N.check("pt_compile_scene_keyed", rc)
     ops = (N.Op * max(1, n_ops.value))()
     aabbs = (N.Aabb * max(1, n_aabb.value))()
     data = np.zeros(n_data.value, dtype=np.float32)
-    rc = L.pt_compile_scene(nodes, len(rows), ops, n_ops.value, ctypes.byref(n_ops), aabbs, n_aabb.value,
-                            ctypes.byref(n_aabb), data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n_data.value,
-                            ctypes.byref(n_data), ctypes.byref(n_check))
-    N.check("pt_compile_scene", rc)
+    rc = L.pt_compile_scene_keyed(nodes, len(rows), keys, ops, n_ops.value, ctypes.byref(n_ops), aabbs, n_aabb.value,
+                                  ctypes.byref(n_aabb), data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                  n_data.value, ctypes.byref(n_data), ctypes.byref(n_check))
+    N.check("pt_compile_scene_keyed", rc)
     return Program(ops, aabbs, n_ops.value, n_aabb.value, n_check.value, data)
 
 

@@ -125,12 +125,32 @@ typedef struct {
 /* Compile a scene tree exactly as SDFEditor::compile allocates data[] slots
  * and check[] indices (sdf_editor.rs:186-246).  Two-call pattern: any output
  * pointer may be NULL, sizes are always written; returns PT_ERR_SIZE if a
- * capacity is too small.  Host-only, no GPU needed. */
+ * capacity is too small.  Host-only, no GPU needed.  Every Float gets its
+ * own slot (the editor draws a fresh random hash per Float,
+ * primitives.rs:12-17,220). */
 int pt_compile_scene(const pt_scene_node *nodes, uint32_t n_nodes,
                      pt_op *ops, uint32_t ops_cap, uint32_t *n_ops,
                      pt_aabb *aabbs, uint32_t aabb_cap, uint32_t *n_aabb,
                      float *data, uint32_t data_cap, uint32_t *n_data,
                      uint32_t *n_check);
+
+/* The identity of one Float: its serde `hash` (u128, primitives.rs:210).
+ * DataArray::get_index (primitives.rs:117-129) gives Floats that share a hash
+ * one data[] slot, holding the first one's value (cloned nodes and edited
+ * JSON files share hashes).  {0, 0} = anonymous: always a fresh slot. */
+typedef struct {
+    uint64_t lo, hi;
+} pt_float_key;
+/* Keys per node: scale, position xyz, rotation xyz, aabb_exaggeration,
+ * size[3], material[18] (a union uses the first 8). */
+#define PT_NODE_FLOATS 29
+/* pt_compile_scene with the Floats' hashes: keys[node * PT_NODE_FLOATS + k]
+ * (NULL = all anonymous, the same as pt_compile_scene). */
+int pt_compile_scene_keyed(const pt_scene_node *nodes, uint32_t n_nodes, const pt_float_key *keys,
+                           pt_op *ops, uint32_t ops_cap, uint32_t *n_ops,
+                           pt_aabb *aabbs, uint32_t aabb_cap, uint32_t *n_aabb,
+                           float *data, uint32_t data_cap, uint32_t *n_data,
+                           uint32_t *n_check);
 
 /* ---------------------------------------------------------------------
  * Render context
@@ -159,6 +179,13 @@ int pt_read_accum(pt_ctx *ctx, float *rgba, size_t bytes);
  * from a caller buffer (resume a progressive render from a saved image, or
  * feed the display pass).  Blocking. */
 int pt_write_accum(pt_ctx *ctx, const float *rgba, size_t bytes);
+/* == the pixel transform of State::save_image (state.rs:277-289), host only:
+ * `rgba` (w*h*4 floats, row 0 = y 0, as pt_read_accum returns it) to the
+ * 8-bit RGBA of image.png, row 0 = top (rows flipped, :283): r, g, b =
+ * (v.powf(1.0 / 2.2) * 255.0) as u8 with Rust's f32 1.0 / 2.2 and libm powf,
+ * a = (v * 255.0) as u8; `as u8` saturates (NaN -> 0).  `out` holds w*h*4
+ * bytes. */
+int pt_save_rgba8(const float *rgba, uint32_t width, uint32_t height, uint8_t *out, size_t bytes);
 /* Device pointer + size of the local image (for external collectives). */
 int pt_accum_device_ptr(pt_ctx *ctx, void **dev_ptr, size_t *bytes);
 int pt_get_size(const pt_ctx *ctx, uint32_t *width, uint32_t *height);
@@ -199,7 +226,9 @@ int pt_display(pt_ctx *ctx, int format, void *out, size_t bytes);
  * rays of a chunk of frames are grouped by their bounds() check set before
  * they are marched), "shade_batch" (state-machine kernels: lanes that must
  * wait before a shading pass runs, 1..64), "bin_samples" (binned kernel:
- * samples per chunk, >= 64; device memory = 176 B per sample), "bin_lanes"
+ * samples per chunk, >= 64; device memory = 152 B per sample, 176 B for
+ * scenes with > 64 check[] entries; default 2^29 samples, at most half of
+ * the device memory this context could hold), "bin_lanes"
  * (binned kernel: 1..4 pipelines, each on its own stream, over which a
  * chunk's frames are split, so one's memory-bound passes overlap another's
  * trace pass), "jit" (1:
@@ -218,7 +247,8 @@ int pt_set_option(pt_ctx *ctx, const char *key, int value);
  * "kernel", "shade_batch",
  * "bin_samples", "bin_lanes", "bin_bytes" (device memory held by the binned
  * pipeline), "trace_ms" / "trace_launches" (device time and count of the last
- * dispatch's binned trace passes, HIP events on each pipeline's stream), "display_ms"
+ * dispatch's binned trace passes, HIP events on each pipeline's stream),
+ * "shade_ms" / "shade_launches" (the same for its shade passes), "display_ms"
  * (device time of the last pt_display's kernel). */
 int pt_get_option(pt_ctx *ctx, const char *key, double *value);
 /* Log of the last failed scene-kernel build ("" if none). */

@@ -48,6 +48,25 @@ class Counters(Structure):
 _lib = None
 
 
+def build_native(out_dir: str) -> str:
+    """The oracle compiled for the host it runs on (-march=native; the
+    shipped build targets x86-64-v3 so it loads on any box).  Same semantics:
+    -ffp-contract=off keeps every rounding step, and the explicit fmaf calls
+    are fused either way.  Used by bench.py's cpu_baseline leg."""
+    out = os.path.join(out_dir, "libpt_oracle_native.so")
+    subprocess.run(["gcc", "-O3", "-march=native", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
+                    "-pthread", "-o", out, os.path.join(HERE, "pt_oracle.c"), "-lm"], check=True)
+    return out
+
+
+def use_library(path: str) -> None:
+    """Load the oracle from ``path`` (before its first use in the process)."""
+    global LIB_PATH, _lib
+    if _lib is not None:
+        raise RuntimeError("oracle library already loaded")
+    LIB_PATH = path
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -57,6 +76,8 @@ def lib():
         vp = ctypes.c_void_p
         L.pto_scene_build.argtypes = [POINTER(Node), c_int, POINTER(vp)]
         L.pto_scene_build.restype = c_int
+        L.pto_scene_build_keyed.argtypes = [POINTER(Node), c_int, POINTER(c_uint64), POINTER(vp)]
+        L.pto_scene_build_keyed.restype = c_int
         L.pto_scene_free.argtypes = [vp]
         L.pto_scene_n_data.argtypes = [vp]
         L.pto_scene_n_check.argtypes = [vp]
@@ -108,7 +129,16 @@ class OracleScene:
         self._nodes = rows_to_nodes(rows)
         self.n_nodes = len(rows)
         h = ctypes.c_void_p()
-        rc = self._L.pto_scene_build(self._nodes, len(rows), ctypes.byref(h))
+        # the Floats' u128 hashes (rows' "keys", 29 per node): shared hashes
+        # share a slot, as DataArray::get_index does
+        self._keys = None
+        if any(r.get("keys") for r in rows):
+            self._keys = (c_uint64 * (2 * 29 * max(1, len(rows))))()
+            for i, r in enumerate(rows):
+                for k, key in enumerate(r.get("keys") or []):
+                    self._keys[2 * (i * 29 + k)] = key & 0xFFFFFFFFFFFFFFFF
+                    self._keys[2 * (i * 29 + k) + 1] = (key >> 64) & 0xFFFFFFFFFFFFFFFF
+        rc = self._L.pto_scene_build_keyed(self._nodes, len(rows), self._keys, ctypes.byref(h))
         if rc != 0:
             raise ValueError(f"pto_scene_build rc={rc}")
         self._h = h

@@ -141,6 +141,8 @@ typedef struct {
 struct pto_scene {
     int n;
     onode *nd;
+    const uint64_t *keys; /* [node][NSLOT][2] Float hashes while compiling, or NULL */
+    int32_t *key_slot;    /* slot of each key position seen so far (first occurrence) */
     int *top, ntop;
     float *data;
     int ndata, cap;
@@ -159,6 +161,23 @@ static int alloc_slot(pto_scene *s, float v) /* primitives.rs:117-129 (DataArray
     return s->ndata++;
 }
 
+/* get_index with the Float's hash: a hash seen before returns its slot (the
+ * slot keeps the first value); a new hash, or {0, 0} (anonymous), appends. */
+static int alloc_keyed(pto_scene *s, float v, int node, int k)
+{
+    if (s->keys) {
+        const uint64_t *key = s->keys + 2 * ((size_t)node * NSLOT + (size_t)k);
+        if (key[0] | key[1]) {
+            for (size_t j = 0; j < (size_t)s->n * NSLOT; j++) {
+                const uint64_t *o = s->keys + 2 * j;
+                if (s->key_slot[j] >= 0 && o[0] == key[0] && o[1] == key[1]) return s->key_slot[j];
+            }
+            return s->key_slot[(size_t)node * NSLOT + (size_t)k] = alloc_slot(s, v);
+        }
+    }
+    return alloc_slot(s, v);
+}
+
 static int size_count(int kind)
 {
     switch (kind) {
@@ -172,34 +191,34 @@ static int size_count(int kind)
 
 /* Transform::compile (data_structures.rs:45-55): scale, position.xyz,
  * (scale again, reused), rotation.xyz, aabb_exaggeration. */
-static void alloc_transform(pto_scene *s, onode *o, const pto_node *src)
+static void alloc_transform(pto_scene *s, onode *o, const pto_node *src, int node)
 {
-    o->slot[SL_SCALE] = alloc_slot(s, src->scale);
-    for (int i = 0; i < 3; i++) o->slot[SL_POS + i] = alloc_slot(s, src->pos[i]);
-    for (int i = 0; i < 3; i++) o->slot[SL_ROT + i] = alloc_slot(s, src->rot[i]);
-    o->slot[SL_EX] = alloc_slot(s, src->aabb_ex);
+    o->slot[SL_SCALE] = alloc_keyed(s, src->scale, node, SL_SCALE);
+    for (int i = 0; i < 3; i++) o->slot[SL_POS + i] = alloc_keyed(s, src->pos[i], node, SL_POS + i);
+    for (int i = 0; i < 3; i++) o->slot[SL_ROT + i] = alloc_keyed(s, src->rot[i], node, SL_ROT + i);
+    o->slot[SL_EX] = alloc_keyed(s, src->aabb_ex, node, SL_EX);
 }
 
 /* Union::compile (containers.rs:143-179) + Shape::compile (:404-440) slot order */
 static void compile_union(pto_scene *s, const pto_node *src, int u, int *aabb_index)
 {
     onode *o = &s->nd[u];
-    alloc_transform(s, o, &src[u]);
+    alloc_transform(s, o, &src[u], u);
     for (int i = 0; i < o->ncu; i++) compile_union(s, src, o->cu[i], aabb_index);
     for (int i = 0; i < o->ncs; i++) {
         int c = o->cs[i];
         onode *sh = &s->nd[c];
-        alloc_transform(s, sh, &src[c]);
+        alloc_transform(s, sh, &src[c], c);
         int nsz = size_count(sh->kind);
-        for (int k = 0; k < nsz; k++) sh->slot[SL_SIZE + k] = alloc_slot(s, src[c].size[k]);
-        for (int k = 0; k < 18; k++) sh->slot[SL_MAT + k] = alloc_slot(s, src[c].mat[k]);
+        for (int k = 0; k < nsz; k++) sh->slot[SL_SIZE + k] = alloc_keyed(s, src[c].size[k], c, SL_SIZE + k);
+        for (int k = 0; k < 18; k++) sh->slot[SL_MAT + k] = alloc_keyed(s, src[c].mat[k], c, SL_MAT + k);
         /* Transform::aabb_check (data_structures.rs:57-66): index bumps for every shape */
         sh->check = sh->aabb ? *aabb_index : -1;
         (*aabb_index)++;
     }
 }
 
-int pto_scene_build(const pto_node *nodes, int n, pto_scene **out)
+int pto_scene_build_keyed(const pto_node *nodes, int n, const uint64_t *keys, pto_scene **out)
 {
     *out = NULL;
     if (n < 0 || (n > 0 && !nodes)) return -1;
@@ -236,8 +255,16 @@ int pto_scene_build(const pto_node *nodes, int n, pto_scene **out)
     }
     if (rc != 0) { pto_scene_free(s); return rc; }
     alloc_slot(s, 6969.69f); /* reset_data_array, primitives.rs:53-56 */
+    if (keys) {
+        s->keys = keys;
+        s->key_slot = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1) * NSLOT);
+        for (size_t j = 0; j < (size_t)(n > 0 ? n : 1) * NSLOT; j++) s->key_slot[j] = -1;
+    }
     int aabb_index = 0;
     for (int t = 0; t < s->ntop; t++) compile_union(s, nodes, s->top[t], &aabb_index);
+    free(s->key_slot);
+    s->key_slot = NULL;
+    s->keys = NULL;
     s->ncheck = aabb_index > 0 ? aabb_index : 1; /* sdf_editor.rs:213 */
     /* bounds(): only direct shapes of header unions, own counter (containers.rs:181-202,442-463) */
     s->bshape = (int *)calloc((size_t)(n > 0 ? n : 1), sizeof(int));
@@ -253,6 +280,11 @@ int pto_scene_build(const pto_node *nodes, int n, pto_scene **out)
     }
     *out = s;
     return 0;
+}
+
+int pto_scene_build(const pto_node *nodes, int n, pto_scene **out)
+{
+    return pto_scene_build_keyed(nodes, n, NULL, out);
 }
 
 void pto_scene_free(pto_scene *s)

@@ -85,6 +85,10 @@ typedef struct pto_scene pto_scene;
 /* Compile the tree: allocate data[] slots exactly like SDFEditor::compile.
  * Returns 0, or -1 on an invalid tree, -2 for Shapes::Plane (NotImplemented). */
 int  pto_scene_build(const pto_node *nodes, int n, pto_scene **out);
+/* With the Floats' u128 hashes, keys[(node * 29 + k) * 2 + {0: lo, 1: hi}]
+ * in the node's slot order (8 transform, 3 size, 18 material); {0, 0} =
+ * anonymous.  Shared hashes share a data[] slot (primitives.rs:117-129). */
+int  pto_scene_build_keyed(const pto_node *nodes, int n, const uint64_t *keys, pto_scene **out);
 void pto_scene_free(pto_scene *s);
 int  pto_scene_n_data(const pto_scene *s);
 int  pto_scene_n_check(const pto_scene *s);

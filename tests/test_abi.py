@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_functions():
     txt = open(os.path.join(ROOT, "include", "pt_abi.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(pt_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(pt_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_every_declared_symbol_is_exported():
@@ -77,3 +77,17 @@ def test_jit_rejects_bad_slots():
     rc = L.pt_jit_compile(prog.ops, prog.n_ops, prog.aabbs, prog.n_aabb,
                           prog.data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 5, log, len(log), None)
     assert rc == N.PT_ERR_INVALID and b"out of range" in log.value
+
+
+def test_comm_argument_errors_without_device():
+    """pt_comm_init / pt_reduce_accum / pt_read_reduced / pt_comm_get_unique_id
+    reject null and out-of-range arguments before any HIP or RCCL call (the
+    state errors with a live context are in test_gpu_parity.py)."""
+    L = N.lib()
+    uid = (ctypes.c_uint8 * N.PT_COMM_ID_BYTES)()
+    assert L.pt_comm_get_unique_id(None) == N.PT_ERR_INVALID
+    assert L.pt_comm_init(None, 2, 0, uid) == N.PT_ERR_INVALID
+    assert L.pt_reduce_accum(None, 0) == N.PT_ERR_INVALID
+    buf = (ctypes.c_float * 4)()
+    assert L.pt_read_reduced(None, buf, 16) == N.PT_ERR_INVALID
+    assert L.pt_accum_device_ptr(None, None, None) == N.PT_ERR_INVALID

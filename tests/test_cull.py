@@ -233,3 +233,16 @@ def test_radius_test_and_bounds_forms(tmp_path):
     assert "uint32_t gapu = 0xffffffffu;" in src
     assert "__ballot(!(gapu > PT_ULP_MARGIN))" in src
     assert re.search(r"w0 \|= ray_box_ulp\(A0, ro\.x, ro\.y, ro\.z, yx, yy, yz, gapu\) \? 0x[0-9a-f]+u : 0u;", src)
+
+
+def test_run_cut_carries_the_underflow_guard(tmp_path):
+    """The trace map's run cut (a cube joining its union by min is skipped
+    when max(q) exceeds the running distance) relies on sdCube >= max(q),
+    which holds in f32 only for max(q) > 2^-60: every run
+    cut the generator emits must carry that guard, like cut_q does."""
+    src, _ = _baked("c3", tmp_path)
+    runs = re.findall(r"const bool cut_r = \(qm > h\d+\.d\)( & \(qm > 0x1p-60f\))?;", src)
+    assert runs, "C3's room cubes take the run cut"
+    assert all(g for g in runs), runs
+    assert not re.search(r"if \(!?\(?qm > h\d+\.d\)", src)
+    assert all("qm > 0x1p-60f" in m for m in re.findall(r"const bool cut_q = [^;]*;", src))

@@ -64,13 +64,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out, mode):
+def _worker(rank, world, port, out, mode, scaling="weak"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     rows = scenes.c2_sphere_box_torus().rows()
     aspect = float(np.float32(W) / np.float32(H))
-    tr = TileSplitRender(OracleRenderer(rows, W, H), rank, world, aspect, reduce=mode)
+    tr = TileSplitRender(OracleRenderer(rows, W, H), rank, world, aspect, reduce=mode, scaling=scaling)
     tr.step(SPP)  # SPP * world frames of this rank's tiles
     tr.step(SPP)
     img = tr.image(0)
@@ -80,15 +80,23 @@ def _worker(rank, world, port, out, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "rccl"), (2, "host"), (3, "host")])
-def test_tile_split_reduce_matches_single_rank(tmp_path, world, mode):
+@pytest.mark.parametrize("world,mode,scaling", [(2, "rccl", "weak"), (2, "host", "weak"), (3, "host", "weak"),
+                                                (2, "rccl", "strong"), (3, "host", "strong")])
+def test_tile_split_reduce_matches_single_rank(tmp_path, world, mode, scaling):
     """mode "rccl" drives the renderer's own reduce (RCCL in PathTracer, gloo
-    in the test double); "host" is TileSplitRender's torch.distributed sum."""
+    in the test double); "host" is TileSplitRender's torch.distributed sum.
+    Weak scaling renders SPP * world frames per step, strong SPP (BASELINE
+    config 4's split of one image)."""
     out = str(tmp_path / "img.npy")
-    mp.spawn(_worker, args=(world, _free_port(), out, mode), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, mode, scaling), nprocs=world, join=True)
     got = np.load(out, allow_pickle=False)
     rows = scenes.c2_sphere_box_torus().rows()
     aspect = float(np.float32(W) / np.float32(H))
     ref = O.OracleScene(rows).render(W, H, O.Constants(0.0, 1, aspect, 1), O.Settings(0, BOUNCES, 1.0, 1.0, 0),
-                                     2 * SPP * world)
+                                     2 * SPP * (world if scaling == "weak" else 1))
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_tile_split_rejects_unknown_scaling():
+    with pytest.raises(ValueError):
+        TileSplitRender(OracleRenderer(scenes.c1_default().rows(), 8, 8), 0, 1, 1.0, scaling="linear")

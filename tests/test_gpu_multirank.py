@@ -1,0 +1,63 @@
+"""The multi-rank HIP path in one GPU test run: bench.py under
+torch.distributed.run with two ranks sharing GPU 0 (PT_BENCH_SHARE_GPU).
+RCCL refuses two ranks on one device, so the ranks reduce over gloo on the
+host (--dist-backend gloo); every rank renders through its own context and
+the library's tile split (pt_set_tiles).  --validate has rank 0 re-render
+every frame in one context and compare the assembled image bit for bit.
+The RCCL reduce itself is covered on one GPU by
+test_gpu_parity.py::test_rccl_single_rank_reduce_and_errors; across GPUs
+only the driver's 8-GPU run reaches it."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(*extra: str, timeout: int = 500) -> dict:
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus", "2",
+           "--no-cpu-baseline", "--dist-backend", "gloo", *extra]
+    env = dict(os.environ, PT_BENCH_SHARE_GPU="1", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("config,scaling", [("c3", "weak"), ("c4", "strong")])
+def test_two_ranks_tile_split_bit_exact(gpu, config, scaling):
+    out = _bench("--config", config, "--width", "480", "--height", "272", "--spp", "4", "--steps", "2",
+                 "--warmup", "1", "--validate")
+    assert out["n_gpus"] == 2 and out["scaling"] == scaling
+    frames = (1 + 2 + 1) * 4 * (2 if scaling == "weak" else 1)  # warm-up, timed steps, the per-launch timing step
+    assert out["validation"] == {"frames": frames, "bit_exact": True}
+    assert out["reduce_ms"] > 0 and out["value"] > 0
+
+
+@pytest.mark.timeout(600)
+def test_two_ranks_strong_config4_leg(gpu):
+    """The default N > 1 line carries BASELINE config 4 split over the ranks
+    (3840x2160, 256 spp) with its reduce timed on its own."""
+    out = _bench("--width", "480", "--height", "272", "--spp", "2", "--steps", "1", "--warmup", "0",
+                 "--c4-steps", "1")
+    leg = out["c4_strong"]
+    assert leg["scaling"] == "strong" and leg["n_gpus"] == 2
+    assert leg["config"]["width"] == 3840 and leg["config"]["spp_per_step"] == 256
+    assert leg["value"] > 0 and leg["reduce_ms"] > 0

@@ -5,6 +5,8 @@ channels.  The semantics contract makes the two bit-exact, so
 the tests also report the bit-exact texel fraction and require it to be 1
 where no transcendental-free difference is expected.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -263,29 +265,144 @@ def test_work_counters_match_oracle(gpu, kernel):
     pt.close()
 
 
-@pytest.mark.parametrize("name,spp", [("c3", 16), ("c2", 16)])
-def test_full_size_tiles_match_oracle(gpu, name, spp):
-    """BASELINE configs at full resolution: 8 random 8x8 tiles, plus every tile
-    holding a non-finite texel (normalize of a zero vector upstream), against
-    the oracle rendering just that tile (rank = tile, nranks = #tiles)."""
-    scene, w, h, _, bounces = scenes.CONFIGS[name]
+def _oracle_tiles(ed, w, h, spp, bounces, tiles):
+    """The oracle's render of each 8x8 tile alone (rank = tile, nranks =
+    #tiles), tiles in parallel (ctypes drops the GIL in pto_render)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    tx, ntiles = (w + 7) // 8, ((w + 7) // 8) * ((h + 7) // 8)
+    aspect = float(np.float32(w) / np.float32(h))
+    osc = O.OracleScene(ed.rows())
+
+    def one(t):
+        ref = osc.render(w, h, O.Constants(0.0, 1, aspect, 1), O.Settings(0, bounces, 1.0, 1.0, 0), spp, rank=t,
+                         nranks=ntiles, threads=1)
+        y0, x0 = (t // tx) * 8, (t % tx) * 8
+        return ref[y0:y0 + 8, x0:x0 + 8].copy()
+
+    with ThreadPoolExecutor(max_workers=16) as ex:
+        return dict(zip(tiles, ex.map(one, tiles)))
+
+
+# BASELINE configs at their full size and spp (C5: 2^31 samples, four 2^29
+# chunks; C4: the 8-GPU image on one GPU)
+FULL_CONFIGS = ["c2", "c3", "c5", "c4"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", FULL_CONFIGS)
+def test_full_size_tiles_match_oracle(gpu, name):
+    """BASELINE configs at full resolution and full spp: 8 random 8x8 tiles,
+    plus the tiles holding a non-finite texel (normalize of a zero vector
+    upstream; at most 16), against the oracle rendering just that tile."""
+    scene, w, h, spp, bounces = scenes.CONFIGS[name]
     ed = scenes.SCENES[scene]()
     st = N.Settings(debug=0, bounces=bounces, scale=1.0, fov=1.0, aabb=0)
     pt = PathTracer(w, h, ed.compile(CompData()), settings=st)
+    pt.set_option("jit_wait", 1)
     aspect = float(np.float32(w) / np.float32(h))
     pt.dispatch(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), spp)
     img = pt.read_image()
+    chunk = pt.get_option("bin_samples")
     pt.close()
+    if name == "c5":
+        assert w * h * spp > 2 * chunk  # the multi-chunk path at full size
     tx, ntiles = (w + 7) // 8, ((w + 7) // 8) * ((h + 7) // 8)
-    bad = {(int(y) // 8) * tx + int(x) // 8 for y, x in np.argwhere(~np.isfinite(img[..., :3]).all(-1))}
-    tiles = sorted(set(np.random.default_rng(11).choice(ntiles, 8, replace=False).tolist()) | bad)
-    osc = O.OracleScene(ed.rows())
-    for t in tiles:
-        ref = osc.render(w, h, O.Constants(0.0, 1, aspect, 1), O.Settings(0, bounces, 1.0, 1.0, 0), spp, rank=t,
-                         nranks=ntiles, threads=8)
+    bad = sorted({(int(y) // 8) * tx + int(x) // 8 for y, x in np.argwhere(~np.isfinite(img[..., :3]).all(-1))})
+    print(f"{name}: {len(bad)} tiles with non-finite texels, mean {np.nanmean(img[..., :3]):.5f}")
+    tiles = sorted(set(np.random.default_rng(11).choice(ntiles, 8, replace=False).tolist()) | set(bad[:16]))
+    for t, ref in _oracle_tiles(ed, w, h, spp, bounces, tiles).items():
         y0, x0 = (t // tx) * 8, (t % tx) * 8
-        a, b = img[y0:y0 + 8, x0:x0 + 8], ref[y0:y0 + 8, x0:x0 + 8]
-        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), t
+        a = img[y0:y0 + 8, x0:x0 + 8]
+        assert np.array_equal(a.view(np.uint32), ref.view(np.uint32)), t
+
+
+@pytest.mark.parametrize("kernel", ALL)
+@pytest.mark.parametrize("bounces", [0, 16, 32])
+def test_parity_bounce_range(gpu, bounces, kernel):
+    """The Settings slider range (path_tracer.rs:160, 0..=32): segments
+    i = 0..=bounces (test_compute.glsl:99), so 1, 17 and 33 passes of the
+    binned pipeline, deep Russian roulette and ping-pong buffers."""
+    gpu_img, ref = _render_pair(scenes.c3_graph32(), 48, 32, 3, bounces, kernel=kernel)
+    rms, exact = _report(gpu_img, ref)
+    assert ref[..., :3].mean() > 0
+    assert rms < RMS_TOL and exact == 1.0, (rms, exact)
+
+
+@pytest.mark.parametrize("kernel", ALL)
+@pytest.mark.parametrize("bounces", [0, 32])
+def test_bounce_heat_map_edges(gpu, bounces, kernel):
+    """debug 3 stores i / bounces (test_compute.glsl:163): at bounces 0 that
+    is 0 / 0 = NaN for a miss and 1 / 0 = +inf for a hit; bit patterns must
+    match the oracle, NaNs included."""
+    gpu_img, ref = _render_pair(scenes.c3_graph32(), 40, 24, 2, bounces, debug=3, kernel=kernel)
+    assert np.array_equal(gpu_img.view(np.uint32), ref.view(np.uint32))
+    if bounces == 0:
+        assert np.isnan(ref[..., 0]).any() and np.isinf(ref[..., 0]).any()
+
+
+@pytest.mark.timeout(600)
+def test_tile_split_2160p_eight_ranks(gpu):
+    """C4's split: eight contexts in one process, each owning
+    the 8x8 tiles t % 8 == rank of the 3840x2160 image; their images summed
+    on the host equal the one-context render bit for bit (non-owned texels
+    are exactly 0)."""
+    scene, w, h, _, bounces = scenes.CONFIGS["c4"]
+    ed = scenes.SCENES[scene]()
+    prog = ed.compile(CompData())
+    st = N.Settings(debug=0, bounces=bounces, scale=1.0, fov=1.0, aabb=0)
+    c = N.Constants(time=0.0, frame=1, aspect=float(np.float32(w) / np.float32(h)), last_clear=1)
+    spp = 16
+    full = PathTracer(w, h, prog, settings=st)
+    full.dispatch(c, spp)
+    want = full.read_image()
+    full.close()
+    acc = np.zeros_like(want)
+    owned = np.zeros(want.shape[:2], np.int32)
+    for r in range(8):
+        p = PathTracer(w, h, prog, settings=st)
+        p.set_tiles(r, 8)
+        p.dispatch(c, spp)
+        part = p.read_image()
+        p.close()
+        nz = (part.view(np.uint32) != 0).any(-1)
+        owned += nz
+        acc += part
+    assert owned.max() == 1  # every texel rendered by at most one rank
+    assert np.array_equal(acc.view(np.uint32), want.view(np.uint32))
+
+
+def test_rccl_single_rank_reduce_and_errors(gpu):
+    """pt_comm_init / pt_reduce_accum / pt_read_reduced through RCCL on one
+    GPU (a 1-rank communicator: the reduce is a copy), plus their argument
+    and state errors."""
+    L = N.lib()
+    ed = scenes.c2_sphere_box_torus()
+    st = N.Settings(debug=0, bounces=3, scale=1.0, fov=1.0, aabb=0)
+    pt = PathTracer(40, 24, ed.compile(CompData()), settings=st)
+    pt.dispatch(N.Constants(time=0.0, frame=1, aspect=float(np.float32(40) / np.float32(24)), last_clear=1), 3)
+    with pytest.raises(N.NativeError) as e:
+        pt.reduce(0)  # before pt_comm_init
+    assert e.value.code == N.PT_ERR_STATE
+    with pytest.raises(N.NativeError) as e:
+        pt.read_reduced()
+    assert e.value.code == N.PT_ERR_STATE
+    uid = PathTracer.comm_unique_id()
+    assert len(uid) == N.PT_COMM_ID_BYTES
+    with pytest.raises(N.NativeError) as e:
+        pt.comm_init(1, 1, uid)  # rank >= nranks
+    assert e.value.code == N.PT_ERR_INVALID
+    pt.comm_init(1, 0, uid)
+    for root in (-1, 1):
+        with pytest.raises(N.NativeError) as e:
+            pt.reduce(root)
+        assert e.value.code == N.PT_ERR_INVALID
+    pt.reduce(0)
+    got = pt.read_reduced()
+    assert np.array_equal(got.view(np.uint32), pt.read_image().view(np.uint32))
+    small = np.zeros(4, np.float32)
+    assert L.pt_read_reduced(pt._ctx, small.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 16) == N.PT_ERR_SIZE
+    pt.close()
 
 
 def test_jit_tier_up_follows_value_edits(gpu):

@@ -116,6 +116,9 @@ def test_div_k_every_numerator(gpu, b):
     """pt_div_k (the baked kernels' division by a scale constant) equals the
     IEEE a / b for all 2^32 numerator patterns: the guarded Markstein range,
     the v_div_fixup specials and the wave fallback."""
-    bad, first = ctypes.c_uint64(), ctypes.c_uint64()
-    assert N.lib().pt_check_div_k(0, ctypes.c_float(b), 0, 0xFFFFFF00, ctypes.byref(bad), ctypes.byref(first)) == N.PT_OK
-    assert bad.value == 0, hex(first.value)
+    # na is a multiple of 256 below 2^32: two calls cover every pattern,
+    # the last 256 (negative NaNs through v_div_fixup) included
+    for a0, na in ((0, 0xFFFFFF00), (0xFFFFFF00, 256)):
+        bad, first = ctypes.c_uint64(), ctypes.c_uint64()
+        assert N.lib().pt_check_div_k(0, ctypes.c_float(b), a0, na, ctypes.byref(bad), ctypes.byref(first)) == N.PT_OK
+        assert bad.value == 0, (hex(a0), hex(first.value))

@@ -194,3 +194,163 @@ def test_deprecated_map_loads_and_pins_c3_room():
                     lambda x: x.material.light_col.vals(), lambda x: [x.material.brightness.val],
                     lambda x: [x.material.specular_chance.val], lambda x: x.material.specular_color.vals()):
             assert get(s) == get(r), s.name
+
+
+SHARED = os.path.join(GOLD, "shared_hashes.json")
+MAT_ORDER = ("color", "brightness", "light_col", "specular_chance", "specular_color", "roughness", "ior",
+             "refract_chance", "refract_roughness", "refract_color")
+
+
+def _v3(d):
+    return [d["x"], d["y"], d["z"]]
+
+
+def _size_floats(cs):
+    (kind, v), = cs.items()
+    return _v3(v) if kind == "Cube" else (v if kind == "Torus" else [v])
+
+
+def _mat_floats(m):
+    out = []
+    for k in MAT_ORDER:
+        out += _v3(m[k]) if "x" in m[k] else [m[k]]
+    return out
+
+
+class _RefData:
+    """DataArray restated from primitives.rs:117-129,153-156 on the JSON."""
+
+    def __init__(self):
+        self.data, self.seen = [np.float32(6969.69)], {}
+
+    def get_index(self, f):
+        if f["hash"] not in self.seen:
+            self.data.append(np.float32(f["val"]))
+            self.seen[f["hash"]] = len(self.data) - 1
+        return self.seen[f["hash"]]
+
+    def refresh(self, f):
+        self.data[self.seen[f["hash"]]] = np.float32(f["val"])
+
+
+def _ref_compile(d):
+    """Slots per node in the reference's Float::compile call order
+    (sdf_editor.rs:186-246 -> containers.rs:143-179,404-440 ->
+    data_structures.rs:45-55 (scale, position, scale again, rotation,
+    exaggeration), :178-194), as the 29-slot rows pto_scene_node_slots
+    reports (a union's size/material slots -1)."""
+    D, rows = _RefData(), []
+
+    def transform(t):
+        s = [D.get_index(t["scale"])] + [D.get_index(f) for f in _v3(t["position"])]
+        D.get_index(t["scale"])
+        s += [D.get_index(f) for f in _v3(t["rotation"])] + [D.get_index(t["aabb_exaggeration"])]
+        return s
+
+    def union(u):
+        rows.append(transform(u["transform"]) + [-1] * 21)
+        for c in u["children_unions"]:
+            union(c)
+        for sh in u["children_shapes"]:
+            s = transform(sh["transform"])
+            sz = [D.get_index(f) for f in _size_floats(sh["current_shape"])]
+            s += sz + [-1] * (3 - len(sz)) + [D.get_index(f) for f in _mat_floats(sh["material"])]
+            rows.append(s)
+
+    for u in d["header_unions"]:
+        union(u)
+    for u in d["header_unions"]:  # aabb_compile re-reads seen hashes only (containers.rs:181-202)
+        for sh in u["children_shapes"]:
+            assert all(f["hash"] in D.seen for f in _v3(sh["transform"]["position"]) + [sh["transform"]["scale"]])
+    return D, rows
+
+
+def _ref_refresh(d, D):
+    """SDFEditor::data_update (sdf_editor.rs:248-252): Union::refresh
+    (transform, shapes, child unions), Shape::refresh (transform, material,
+    size), Transform::refresh (position, rotation, scale, exaggeration)."""
+    def transform(t):
+        for f in _v3(t["position"]) + _v3(t["rotation"]) + [t["scale"], t["aabb_exaggeration"]]:
+            D.refresh(f)
+
+    def union(u):
+        transform(u["transform"])
+        for sh in u["children_shapes"]:
+            transform(sh["transform"])
+            for f in _mat_floats(sh["material"]) + _size_floats(sh["current_shape"]):
+                D.refresh(f)
+        for c in u["children_unions"]:
+            union(c)
+
+    for u in d["header_unions"]:
+        union(u)
+
+
+def test_shared_hashes_share_slots_like_get_index():
+    """Floats that share a hash share one data[] slot holding the first
+    value (primitives.rs:117-129): product compiler and oracle both match the
+    restatement of the reference's compile order on the fixture."""
+    d = json.load(open(SHARED))
+    D, ref_rows = _ref_compile(d)
+    ed = SDFEditor.from_json(d)
+    cd = CompData()
+    prog = ed.compile(cd)
+    assert len(prog.data) == len(D.data) < len(scenes.c2_sphere_box_torus().compile(CompData()).data) + 29 + 1
+    assert np.array_equal(prog.data.view(np.uint32), np.array(D.data, np.float32).view(np.uint32))
+    rows = ed.rows()
+    osc = O.OracleScene(rows)
+    assert np.array_equal(osc.data().view(np.uint32), prog.data.view(np.uint32))
+    ops = [o for o in prog.op_dicts() if o["opcode"] != N.PT_OP_UNION_END]
+    assert len(ops) == len(rows) == len(ref_rows)
+    for i, (o, r) in enumerate(zip(ops, ref_rows)):
+        got = [o["scale"], *o["position"], *o["rotation"], o["aabb_exaggeration"]]
+        assert got == r[:8], i
+        assert osc.node_slots(i)[0][:8] == r[:8], i
+        if o["opcode"] == N.PT_OP_SHAPE:
+            nsz = 3 - r[8:11].count(-1)
+            assert o["size"][:nsz] == r[8:8 + nsz] and o["material"] == r[11:29], i
+            assert osc.node_slots(i)[0][8:8 + nsz] == r[8:8 + nsz] and osc.node_slots(i)[0][11:29] == r[11:29]
+    # the clone shares every slot with the box; the clone's own position value is dropped
+    box, clone = ops[2], ops[3]
+    assert {k: v for k, v in box.items() if k != "check"} == {k: v for k, v in clone.items() if k != "check"}
+    assert (box["check"], clone["check"]) == (1, 2)  # Transform::aabb_check counts every shape
+    assert prog.data[box["position"][0]] == np.float32(0.8)
+    assert box["rotation"][0] == box["rotation"][2] != box["rotation"][1]
+    sphere = ops[1]
+    assert box["material"][8:11] == sphere["material"][0:3]
+    # the Python DataArray registers the same slots (refresh targets)
+    for i, r in enumerate(ref_rows):
+        assert all(cd.data_array.data[s] == D.data[s] for s in r if s >= 0)
+
+
+def test_shared_hashes_refresh_writes_like_the_reference():
+    """A value-only refresh with shared hashes: every Float writes its slot
+    in the reference's refresh order, so the last writer wins (the clone's
+    -1.6 replaces the box's 0.8)."""
+    d = json.load(open(SHARED))
+    ed = SDFEditor.from_json(d)
+    cd = CompData()
+    ed.compile(cd)
+    ed.header_unions[0].children_shapes[0].material.color.set((0.3, 0.6, 0.9))  # shared with the box's spec colour
+    ed.header_unions[0].children_shapes[1].transform.rotation.x.set(0.45)  # shared with its rotation z
+    ed.data_update(cd)
+    d2 = ed.to_json()
+    D, _ = _ref_compile(d)
+    _ref_refresh(d2, D)
+    assert np.array_equal(cd.data_array.as_array().view(np.uint32), np.array(D.data, np.float32).view(np.uint32))
+    prog = ed.compile(CompData())
+    box = [o for o in prog.op_dicts() if o["opcode"] == N.PT_OP_SHAPE][1]
+    assert cd.data_array.data[box["position"][0]] == np.float32(-1.6)
+    # rotation z's Float still holds its own (stale) value: its refresh runs
+    # after x's and writes it back over the shared slot
+    assert cd.data_array.data[box["rotation"][0]] == np.float32(ed.header_unions[0].children_shapes[1]
+                                                                 .transform.rotation.z.val)
+
+
+def test_keyed_compile_without_keys_is_the_plain_compile():
+    rows = scenes.c3_graph32().rows()
+    for r in rows:
+        r.pop("keys")
+    a = compile_rows(rows)
+    b = scenes.c3_graph32().compile(CompData())
+    assert np.array_equal(a.data, b.data) and a.op_dicts() == b.op_dicts()
