@@ -719,6 +719,25 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 map_point(TAPS ? state : int(ST_MARCH), step, ro, rd, t, qx, qy, qz);
                 uint64_t live = 0;  // (the taps' live mask: unused here)
                 const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, __builtin_inff(), __builtin_inff(), live, st);
+#if defined(PT_EXP_VALUPAD) || defined(PT_EXP_SALUPAD)  // timing probes: N extra independent VALU / SALU per map
+                {
+#ifdef PT_EXP_VALUPAD
+                    float a0 = qx, a1 = qy, a2 = qz, a3 = t;
+#pragma unroll
+                    for (int k = 0; k < PT_EXP_VALUPAD / 4; ++k)
+                        __asm__ volatile("v_add_f32 %0, %0, 1.0\n v_add_f32 %1, %1, 1.0\n v_add_f32 %2, %2, 1.0\n"
+                                         " v_add_f32 %3, %3, 1.0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+                    __asm__ volatile("" ::"v"(a0), "v"(a1), "v"(a2), "v"(a3));
+#endif
+#ifdef PT_EXP_SALUPAD
+                    uint32_t s0 = uint32_t(__builtin_amdgcn_readfirstlane(step)), s1 = s0 + 1u;
+#pragma unroll
+                    for (int k = 0; k < PT_EXP_SALUPAD / 2; ++k)
+                        __asm__ volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1));
+                    __asm__ volatile("" ::"s"(s0), "s"(s1));
+#endif
+                }
+#endif
                 after_map<ST, !TAPS>(h, state, step, t, ro, rd, mat, dv0, dv1, dv2, st);
                 if constexpr (!TAPS) {
                     if (state == ST_NORMAL) {  // hit: the shade pass takes the taps
