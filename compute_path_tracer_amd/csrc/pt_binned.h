@@ -701,6 +701,11 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             }
             wtake += take;
             if (wtake == wcnt) stage();  // wcnt = 0: no rays left for this wave
+#ifdef PT_REFILL_LGKM
+            // the window's LDS reads have landed before map() starts, so the
+            // shape blocks need no lgkmcnt waits of their own
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+#endif
         }
         const bool more = wcnt != 0u;
         tm = st.lap(PT_ST_CYC_REFILL, tm);

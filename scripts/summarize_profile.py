@@ -110,6 +110,9 @@ def main(tag: str, src: str = None) -> None:
            "bench_config": bench_line["config"] if bench_line else None,
            "bench_value": bench_line["value"] if bench_line else None,
            "bench_kernel_ms_hip_events": bench_line["roofline"]["kernel_ms_per_launch"] if bench_line else None,
+           "bench_shade_ms_hip_events": (bench_line["roofline"].get("shade") or {}).get("ms_per_launch")
+           if bench_line else None,
+           "shade_avg_s_kernel_trace": avg_s("pt_bin_shade_t_jit"),
            "other_kernels": others}
     with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
@@ -123,6 +126,9 @@ def main(tag: str, src: str = None) -> None:
                   f"{out['bench_kernel_ms_hip_events']} ms; rocprofv3 over the same launches "
                   f"({hot} + pt_bin_trace_g_jit, launch-weighted): "
                   f"{trace_avg * 1e3 if trace_avg else None} ms", "",
+              f"HIP-event time per shade launch inside bench.py: {out['bench_shade_ms_hip_events']} ms; "
+              f"rocprofv3 (pt_bin_shade_t_jit): "
+              f"{out['shade_avg_s_kernel_trace'] * 1e3 if out['shade_avg_s_kernel_trace'] else None} ms", "",
               "## Hot kernel counters (per launch)", "", f"kernel: {meta}", ""]
     for k, v in sorted(per_launch.items()):
         lines.append(f"- {k}: {v:.6g}")
