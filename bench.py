@@ -526,7 +526,7 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
                      "traffic_source": None,
                      "algorithmic_flops_per_sample": round(flops_step / max(1, st["samples"]), 1),
                      "kernel_flops_per_launch": round(k_flops / launches),
-                     "kernel_scope": "trace passes (the first with its camera rays and primary bounds()) : march "
+                     "kernel_scope": "trace passes (the first with its camera rays and primary bounds()): march "
                                      "map() work + 10 per step" if gen_trace else "trace passes: march",
                      "kernel_ms_per_launch": round(k_ms, 3), "kernel_launches_per_step": launches,
                      "dispatch_ms_per_step": round(d_ms, 3),

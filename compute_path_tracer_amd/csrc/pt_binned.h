@@ -36,6 +36,14 @@
 #define PT_BIN_NONE 0xffffffffu
 #define PT_AUX_MISS 0xffffffffu  // trace -> shade: PtRay q2.w of a position whose segment missed
 #define PT_BIN_BLOCK 256  // threads per block of the gen / bounds / scatter kernels
+// A pass's control words (PtPass.ctrl): [0] = its ray count, and the trace
+// pass's run cursors, one per share of the pass (PT_RUN_SHARDS, one per XCD),
+// each on its own 128-byte line.
+#ifndef PT_RUN_SHARDS
+#define PT_RUN_SHARDS 8
+#endif
+#define PT_CTRL_CURSOR(k) (32u * (1u + uint32_t(k)))
+#define PT_CTRL_STRIDE (32u * (1u + uint32_t(PT_RUN_SHARDS)))
 #ifndef PT_SCATTER_ITEMS
 #define PT_SCATTER_ITEMS 16
 #endif
@@ -67,7 +75,7 @@ struct PtPass {
     uint32_t *idx;          // rin slots in bin order
     uint32_t *hist;         // [PT_BINS] counts, zero outside gen/bounds -> scan
     uint32_t *offs;         // [PT_BINS] scatter cursors
-    uint32_t *ctrl;         // this pass: [0] binned rays, [1] trace run cursor
+    uint32_t *ctrl;         // this pass: [0] binned rays, [PT_CTRL_CURSOR(k)] trace run cursors
     const uint32_t *n_src;  // rin slots (bounds / scatter), null: n_src_const
     float4 *color;          // [frames][n_pix] sample colours
     float4 *hitn;           // trace -> shade: check[] bits 64..127 of a hit (.zw; scenes with > 64 entries)
@@ -431,10 +439,8 @@ __device__ __forceinline__ void bin_scan_body(const PtPass &P) {
         o4[j] = o;
         h4[j] = make_uint4(0u, 0u, 0u, 0u);
     }
-    if (t == PT_SCAN_THREADS - 1) {
-        P.ctrl[0] = inc;
-        P.ctrl[1] = 0u;
-    }
+    if (t == PT_SCAN_THREADS - 1) P.ctrl[0] = inc;
+    if (t < PT_RUN_SHARDS) P.ctrl[PT_CTRL_CURSOR(t)] = 0u;
 }
 
 // scatter: ray slots into bin order.  Per block tile, the slots of one bin
@@ -541,27 +547,44 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     const uint32_t rmax = uint32_t(P.run_max);
     uint32_t R = n / (gridDim.x * 8u);
     R = R < 64u ? 64u : (R > rmax ? rmax : (R + 63u) & ~63u);
-    auto run_len = [&](uint32_t) { return R; };
-#ifdef PT_EXP_STATICRUN  // timing experiment: runs dealt round-robin, no cursor atomics
-    uint32_t run_k = 0u;
-    auto take = [&](uint32_t len) { return (blockIdx.x + (run_k++) * gridDim.x) * len; };
-#else
-    auto take = [&](uint32_t len) { return atomicAdd(&P.ctrl[1], len); };
-#endif
+    // Run cursors: one per share of the pass (PT_RUN_SHARDS contiguous
+    // shares, whole windows).  A wave takes runs from the share of its
+    // workgroup's XCD (blockIdx % 8: workgroups go to the XCDs round-robin)
+    // and, once that share is used up, from the next ones.  One device-scope
+    // atomic word saturates at ~88 dequeues per us (MI355X_MICROARCH.md,
+    // "dequeue"): the first pass of a C2 render asks for ~2.6e5 runs in ~3 ms.
+    uint32_t shard = blockIdx.x % PT_RUN_SHARDS, tried = 0u;
+    auto shard_lo = [&](uint32_t k) -> uint32_t {
+        return k >= PT_RUN_SHARDS ? n : uint32_t((uint64_t(n >> 6) * k / PT_RUN_SHARDS) << 6);
+    };
+    // (lane 0) reserve a run of `len` positions: its start, and its end in
+    // `end`; start == end == n once every share is used up
+    auto take = [&](uint32_t len, uint32_t &end) -> uint32_t {
+        while (tried < PT_RUN_SHARDS) {
+            const uint32_t lo = shard_lo(shard), hi = shard_lo(shard + 1u);
+            const uint32_t b = lo + atomicAdd(&P.ctrl[PT_CTRL_CURSOR(shard)], len);
+            if (b < hi) {
+                end = b + len < hi ? b + len : hi;
+                return b;
+            }
+            shard = (shard + 1u) % PT_RUN_SHARDS;
+            ++tried;
+        }
+        end = n;
+        return n;
+    };
 
     // runs [run_cur, run_end); the next run is reserved one run ahead
-    uint32_t nxt = 0u, nxt_len = run_len(0u);
-    if (lane == 0) nxt = take(nxt_len);
-    uint32_t run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt))), run_end = 0u;
-    run_end = run_cur < n ? (run_cur + nxt_len < n ? run_cur + nxt_len : n) : run_cur;
-    nxt_len = run_len(run_cur);
-    if (lane == 0 && run_cur < n) nxt = take(nxt_len);
+    uint32_t nxt = 0u, nxt_end = 0u;
+    if (lane == 0) nxt = take(R, nxt_end);
+    uint32_t run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt)));
+    uint32_t run_end = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt_end)));
+    if (lane == 0 && run_cur < n) nxt = take(R, nxt_end);
     auto next_window = [&](uint32_t &b, uint32_t &c) {
         if (run_cur >= run_end) {
             run_cur = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt)));
-            run_end = run_cur < n ? (run_cur + nxt_len < n ? run_cur + nxt_len : n) : run_cur;
-            nxt_len = run_len(run_cur);
-            if (lane == 0 && run_cur < n) nxt = take(nxt_len);
+            run_end = uint32_t(__builtin_amdgcn_readfirstlane(int(nxt_end)));
+            if (lane == 0 && run_cur < n) nxt = take(R, nxt_end);
         }
         b = run_cur;
         c = run_end - run_cur < 64u ? run_end - run_cur : 64u;

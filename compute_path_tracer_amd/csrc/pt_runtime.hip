@@ -697,7 +697,7 @@ static void free_bin(pt_ctx *c) {
 
 // Buffers for `lanes` pipelines of `samples` samples each.
 static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
-    const size_t words = 4 * (passes + 1);
+    const size_t words = size_t(PT_CTRL_STRIDE) * (passes + 1);
     // (mask_hi, check[] bits 64..127, exists only for scenes with > 64 entries)
     const bool hi_ok = c->n_check <= 64 || (c->n_lanes > 0 && c->lane[0].mask_hi != nullptr);
     if (samples <= c->bin_cap && words <= c->ctrl_words && lanes <= c->n_lanes && hi_ok) return PT_OK;
@@ -890,11 +890,12 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         const bool full_tiles = L.width % PT_TILE == 0 && L.height % PT_TILE == 0 && L.debug == 0;
         for (int i = 0; i < nl && !gen_bin && full_tiles; ++i) {
             P[i].gen_order = 1;
-            // ctrl words 0-1 = {count, 0}: stream-ordered fills, no host
-            // buffer whose lifetime the copy would have to outlast
+            // pass 0's control words = {count, run cursors 0}: stream-ordered
+            // fills, no host buffer whose lifetime the copy would have to outlast
+            HIPCHK(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->lane[i].ctrl), 0, PT_CTRL_STRIDE,
+                                        c->lane[i].stream));
             HIPCHK(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->lane[i].ctrl), int(P[i].n_src_const), 1,
                                         c->lane[i].stream));
-            HIPCHK(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->lane[i].ctrl + 1), 0, 1, c->lane[i].stream));
         }
         static const int gen_jit = [] {  // A/B knob: PT_GEN_JIT=0 keeps the ahead-of-time gen kernel
             const char *v = std::getenv("PT_GEN_JIT");
@@ -926,7 +927,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             PtPass S = P[i];
             S.bounce = k;
             S.rin = c->lane[i].ray[(k + 1) & 1];
-            S.n_src = c->lane[i].ctrl + 4 * k;
+            S.n_src = c->lane[i].ctrl + size_t(PT_CTRL_STRIDE) * k;
             if (!stats) HIPCHK(c, record_event(c->slog, c->lane[i].stream));
             if (taps_shade) {
                 void *args[] = {&S};
@@ -950,8 +951,8 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 p.bounce = k;
                 p.rin = l.ray[k & 1];
                 p.rout = l.ray[(k + 1) & 1];
-                p.ctrl = l.ctrl + 4 * k;
-                p.n_src = k == 0 ? nullptr : l.ctrl + 4 * (k - 1);
+                p.ctrl = l.ctrl + size_t(PT_CTRL_STRIDE) * k;
+                p.n_src = k == 0 ? nullptr : l.ctrl + size_t(PT_CTRL_STRIDE) * (k - 1);
                 if (k > 0 || !p.gen_order) {
                     pt_launch_bin(PtBinStage::Scan, p, stats, 1, l.stream);
                     pt_launch_bin(PtBinStage::Scatter, p, stats, scatter_grid(k == 0 ? p.n_src_const : c->bin_cap),

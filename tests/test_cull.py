@@ -139,7 +139,9 @@ def test_bounds_match_restatement(scene, tmp_path):
             # that have a running parent distance to test against
             static = all(nodes[k]["op"] == N.PT_OP_SHAPE and nodes[k]["combine"] != N.PT_COMBINE_SUBTRACTION
                          for k in range(i + 1, j)) and e["combine"] == N.PT_COMBINE_UNION and not fresh_parent[i]
-            assert (f"* B{i}.pad[0];" in src) == static, i
+            # (the trace map's target carries the NaN-folded point bound:
+            # `pb ? h.d * B.pad[0] : NaN`, PT_JIT_PBNAN)
+            assert (f"* B{i}.pad[0]" in src) == static, i
             eligible = static or (fresh_parent[i] and use_bnd.get(i, False) and all(
                 nodes[k]["op"] == N.PT_OP_SHAPE and nodes[k]["combine"] != N.PT_COMBINE_SUBTRACTION
                 for k in range(i + 1, j)) and e["combine"] == N.PT_COMBINE_UNION)
@@ -228,7 +230,14 @@ def test_radius_test_and_bounds_forms(tmp_path):
     test), and the shade kernels' straight-line bounds() decides its slab
     tests by the ulp margin, one select per box bit."""
     src, _ = _baked("c3", tmp_path)
-    cuts = re.findall(r"const bool cut = pb\d+ (&&?) \(cl \* 0x1\.ff8p-1f > cK \* cK\);", src)
+    trace, taps = src[:src.index("struct JitMapB")], src[src.index("struct JitMapB"):]
+    # the trace map: the point bound folded into the union's target as NaN
+    # (PT_JIT_PBNAN), the target's margin term hoisted per union
+    assert re.search(r"const float tg\d+ = pb\d+ \? h\d+\.d \* B\d+\.pad\[0\] : __builtin_nanf\(\"\"\);", trace)
+    assert re.search(r"const float cT\d+ = __builtin_fmaf\(fabsf\(tg\d+\), 0x1p-12f, tg\d+\);", trace)
+    assert re.findall(r"const bool cut = cl \* 0x1\.ff8p-1f > cK \* cK;", trace)
+    assert not re.findall(r"const bool cut = pb\d+", trace)
+    cuts = re.findall(r"const bool cut = pb\d+ (&&?) \(cl \* 0x1\.ff8p-1f > cK \* cK\);", taps)
     assert cuts and set(cuts) == {"&"}, set(cuts)
     assert "uint32_t gapu = 0xffffffffu;" in src
     assert "__ballot(!(gapu > PT_ULP_MARGIN))" in src
