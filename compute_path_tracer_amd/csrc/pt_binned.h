@@ -91,7 +91,10 @@ struct PtPass {
     int32_t gen_trace;      // first pass without a gen pass (scene kernels, generation order): the trace
                             // pass makes each window's camera rays and bounds() itself, a miss zeroes its
                             // colour slot, and the shade pass stores (not adds) the first segment's emission
+    uint32_t *scan_ctrl;    // shade: non-null = the next pass's control words; the block that finishes last
+                            // scans the histogram into offs and sets them (no separate scan launch)
 };
+#define PT_CTRL_TICKET 16u  // control word counting a shade pass's finished blocks (fused scan)
 
 namespace pt {
 
@@ -241,6 +244,49 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
     }
     if (!P.gen_order) hist_flush(lh, P.hist);
     flush_stats<ST>(L, st);
+}
+
+// The histogram scan of bin_scan_body, done by the shade pass's last block
+// to finish (a ticket on scan_ctrl[PT_CTRL_TICKET]) instead of a one-wave
+// kernel launched after it: that launch needed a free wave slot while the
+// other pipeline's shade blocks filled every CU (up to 0.4 ms per pass on a
+// C2 render).  The counts are read (and zeroed) with atomic exchanges -- the
+// other blocks' flushes are device-scope atomics.  lds: PT_BIN_BLOCK words.
+__device__ __forceinline__ void bin_scan_fused(const PtPass &P, uint32_t *lds) {
+    __shared__ uint32_t last;
+    __threadfence();  // this thread's histogram atomics before the block's ticket
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(P.scan_ctrl + PT_CTRL_TICKET, 1u) == gridDim.x - 1u ? 1u : 0u;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    constexpr int PER = PT_BINS / PT_BIN_BLOCK;
+    const int t = int(threadIdx.x);
+    uint32_t v[PER], sum = 0u;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        v[j] = atomicExch(P.hist + t * PER + j, 0u);  // (zeroed for the next pass)
+        sum += v[j];
+    }
+    uint32_t inc = sum;  // inclusive prefix within the wave
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t x = uint32_t(__shfl_up(int(inc), off, 64));
+        if ((t & 63) >= off) inc += x;
+    }
+    if ((t & 63) == 63) lds[t >> 6] = inc;  // wave totals
+    __syncthreads();
+    uint32_t base = 0u;
+    for (int w = 0; w < (t >> 6); ++w) base += lds[w];
+    uint32_t run = base + inc - sum;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        P.offs[t * PER + j] = run;
+        run += v[j];
+    }
+    if (t == PT_BIN_BLOCK - 1) P.scan_ctrl[0] = run;  // the next pass's ray count
+    if (t < PT_RUN_SHARDS) P.scan_ctrl[PT_CTRL_CURSOR(t)] = 0u;
+    if (t == 0) P.scan_ctrl[PT_CTRL_TICKET] = 0u;
 }
 
 // shade: every hit the last trace pass wrote (positions marked HIT) is
@@ -396,6 +442,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         else shade_one(i, q0, q1, q2, q3, hi);
     }
     hist_flush(lh, P.hist);
+    if (P.scan_ctrl) bin_scan_fused(P, lh);
     flush_stats<ST>(L, st);
     if constexpr (!TAPS) flush_stats<ST>(L, stt, PT_ST_COUNT);
 }

@@ -730,8 +730,10 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
         if (!c->join_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming));
         c->lane[i].stream = c->xstream[i];
     }
-    for (int i = 0; i < lanes; ++i)
+    for (int i = 0; i < lanes; ++i) {
         HIPCHK(c, hipMemsetAsync(c->lane[i].hist, 0, PT_BINS * sizeof(uint32_t), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->lane[i].ctrl, 0, words * sizeof(uint32_t), c->stream));  // (fused-scan tickets)
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->n_lanes = lanes;
     c->bin_cap = samples;
@@ -921,6 +923,11 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 HIPCHK(c, hipGetLastError());
             }
         }
+        // PT_FUSED_SCAN=0: the histogram scan as its own one-wave launch (A/B)
+        static const int fused_scan = [] {
+            const char *v = std::getenv("PT_FUSED_SCAN");
+            return v ? std::atoi(v) : 1;
+        }();
         // shade the hits trace pass k wrote into ray[(k + 1) & 1]: ended paths
         // store their colour, the rest get their next ray, bounds() and bin
         auto shade = [&](int i, int k) -> int {
@@ -928,6 +935,8 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             S.bounce = k;
             S.rin = c->lane[i].ray[(k + 1) & 1];
             S.n_src = c->lane[i].ctrl + size_t(PT_CTRL_STRIDE) * k;
+            // the next pass's histogram scan in the shade pass's last block
+            S.scan_ctrl = (fused_scan && k + 1 < passes) ? c->lane[i].ctrl + size_t(PT_CTRL_STRIDE) * (k + 1) : nullptr;
             if (!stats) HIPCHK(c, record_event(c->slog, c->lane[i].stream));
             if (taps_shade) {
                 void *args[] = {&S};
@@ -954,7 +963,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 p.ctrl = l.ctrl + size_t(PT_CTRL_STRIDE) * k;
                 p.n_src = k == 0 ? nullptr : l.ctrl + size_t(PT_CTRL_STRIDE) * (k - 1);
                 if (k > 0 || !p.gen_order) {
-                    pt_launch_bin(PtBinStage::Scan, p, stats, 1, l.stream);
+                    if (k == 0 || !fused_scan) pt_launch_bin(PtBinStage::Scan, p, stats, 1, l.stream);
                     pt_launch_bin(PtBinStage::Scatter, p, stats, scatter_grid(k == 0 ? p.n_src_const : c->bin_cap),
                                   l.stream);
                     HIPCHK(c, hipGetLastError());
