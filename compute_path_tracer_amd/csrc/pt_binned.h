@@ -692,8 +692,42 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     float dv0 = 0.0f, dv1 = 0.0f, dv2 = 0.0f;
     Check ck{0ull, 0ull};
 
+    auto hand_on = [&]() {
+        if (state == ST_SHADE) {
+            if (step < 0) {
+                if (L.debug == 3) {  // bounce-count view
+                    const pt_f3 c = final_color(L.debug, P.bounce, L.bounces, pt_f3{0.0f, 0.0f, 0.0f});
+                    P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
+                }
+                P.rout[pos].q[2] = make_uint4(0u, 0u, sid, PT_AUX_MISS);
+                if constexpr (GEN) P.color[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // (no gen pass zeroed it)
+            } else {
+                if constexpr (TAPS) {  // normal differences
+                    store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
+                              make_uint4(__float_as_uint(dv0), __float_as_uint(dv1), __float_as_uint(dv2), 0u));
+                } else {  // hit point + check[] + tap bound + material (bin_shade_body)
+                    store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
+                              make_uint4(uint32_t(ck.lo), uint32_t(ck.lo >> 32), __float_as_uint(dv0), 0u));
+                    if (wide_of<Map>(P))
+                        P.hitn[pos] = make_float4(0.0f, 0.0f, __uint_as_float(uint32_t(ck.hi)),
+                                                  __uint_as_float(uint32_t(ck.hi >> 32)));
+                }
+            }
+            state = ST_FREE;
+        }
+    };
+
     for (;;) {
         uint64_t tm = st.clk();
+#ifdef PT_DEFER_STORE
+        // ---- 0. finished segments handed on together with the refill
+        {
+            const uint64_t donem = __ballot(state == ST_FREE || state == ST_SHADE);
+            if (donem != 0ull && (__popcll(donem) >= P.refill_min ||
+                                  __ballot(state == ST_MARCH || state == ST_NORMAL) == 0ull))
+                hand_on();
+        }
+#endif
         // ---- 1. refill free lanes from the staging window --------------
         const uint64_t freem = __ballot(state == ST_FREE);
         if (freem != 0ull && wcnt != 0u &&
@@ -826,29 +860,12 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
 
         // ---- 3. hand finished segments on: a miss ends the path (its
         // colour slot already holds its radiance), a hit goes to the shade
-        // pass as one 64 B record (PtRay)
-        if (state == ST_SHADE) {
-            if (step < 0) {
-                if (L.debug == 3) {  // bounce-count view
-                    const pt_f3 c = final_color(L.debug, P.bounce, L.bounces, pt_f3{0.0f, 0.0f, 0.0f});
-                    P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
-                }
-                P.rout[pos].q[2] = make_uint4(0u, 0u, sid, PT_AUX_MISS);
-                if constexpr (GEN) P.color[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // (no gen pass zeroed it)
-            } else {
-                if constexpr (TAPS) {  // normal differences
-                    store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
-                              make_uint4(__float_as_uint(dv0), __float_as_uint(dv1), __float_as_uint(dv2), 0u));
-                } else {  // hit point + check[] + tap bound + material (bin_shade_body)
-                    store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
-                              make_uint4(uint32_t(ck.lo), uint32_t(ck.lo >> 32), __float_as_uint(dv0), 0u));
-                    if (wide_of<Map>(P))
-                        P.hitn[pos] = make_float4(0.0f, 0.0f, __uint_as_float(uint32_t(ck.hi)),
-                                                  __uint_as_float(uint32_t(ck.hi >> 32)));
-                }
-            }
-            state = ST_FREE;
-        }
+        // pass as one 64 B record (PtRay).  PT_DEFER_STORE: at the next
+        // refill instead (step 0), so the stores' branch runs once for
+        // several finished lanes rather than in nearly every iteration
+#ifndef PT_DEFER_STORE
+        hand_on();
+#endif
         tm = st.lap(PT_ST_CYC_SHADE, tm);
         if (!more && __ballot(state != ST_FREE) == 0ull) break;
     }
