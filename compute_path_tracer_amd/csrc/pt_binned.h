@@ -196,7 +196,6 @@ __device__ __forceinline__ void hist_flush(const uint32_t *lh, uint32_t *hist) {
     for (int b = int(threadIdx.x); b < PT_BINS; b += int(blockDim.x))
         if (lh[b] != 0u) atomicAdd(&hist[b], lh[b]);
 }
-
 // local pixel slot -> image coordinates (cyclic tile ownership, as pt_wave.h)
 __device__ __forceinline__ void pixel_of(const PtLaunch &L, uint32_t pl, int &x, int &y) {
     const int k = int(pl >> 6), p = int(pl & 63u);
@@ -254,12 +253,15 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
 // other blocks' flushes are device-scope atomics.  lds: PT_BIN_BLOCK words.
 __device__ __forceinline__ void bin_scan_fused(const PtPass &P, uint32_t *lds) {
     __shared__ uint32_t last;
-    __threadfence();  // this thread's histogram atomics before the block's ticket
+    // the block's histogram atomics performed before its ticket: a wait for
+    // the thread's outstanding vector-memory operations (no-return atomics
+    // stay counted in vmcnt until done), not a release fence, whose L2
+    // write-back in every block cost a C2 render 45 %
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     __syncthreads();
     if (threadIdx.x == 0) last = atomicAdd(P.scan_ctrl + PT_CTRL_TICKET, 1u) == gridDim.x - 1u ? 1u : 0u;
     __syncthreads();
     if (!last) return;
-    __threadfence();
     constexpr int PER = PT_BINS / PT_BIN_BLOCK;
     const int t = int(threadIdx.x);
     uint32_t v[PER], sum = 0u;
