@@ -923,10 +923,13 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 HIPCHK(c, hipGetLastError());
             }
         }
-        // PT_FUSED_SCAN=0: the histogram scan as its own one-wave launch (A/B)
+        // PT_FUSED_SCAN=1: the next pass's histogram scan in the shade
+        // pass's last block (bin_scan_fused) instead of a one-wave launch.
+        // Equal within box noise on C2 and C3 (`DESIGN.md` 8b), so the
+        // kernel boundary, whose ordering needs no argument, stays the default.
         static const int fused_scan = [] {
             const char *v = std::getenv("PT_FUSED_SCAN");
-            return v ? std::atoi(v) : 1;
+            return v ? std::atoi(v) : 0;
         }();
         // shade the hits trace pass k wrote into ray[(k + 1) & 1]: ended paths
         // store their colour, the rest get their next ray, bounds() and bin
