@@ -433,8 +433,21 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     // Nearly every position holds a hit (misses end in the trace pass), so
     // each thread takes one position and loads its whole record (a miss
     // marks its record's q2): one memory round trip.
+#ifdef PT_SHADE_PREFETCH  // A/B: the next position's record loaded before this one is shaded
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint4 p0 = make_uint4(0u, 0u, 0u, 0u), p1 = p0, p2 = p0, p3 = p0;
+    if (i < n) p0 = P.rin[i].q[0], p1 = P.rin[i].q[1], p2 = P.rin[i].q[2], p3 = P.rin[i].q[3];
+    for (; i < n; i += stride) {
+        const uint4 q0 = p0, q1 = p1, q2 = p2, q3 = p3;
+        if (i + stride < n) {
+            const PtRay *nx = P.rin + i + stride;
+            p0 = nx->q[0], p1 = nx->q[1], p2 = nx->q[2], p3 = nx->q[3];
+        }
+#else
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint4 q0 = P.rin[i].q[0], q1 = P.rin[i].q[1], q2 = P.rin[i].q[2], q3 = P.rin[i].q[3];
+#endif
         uint2 hi = make_uint2(0u, 0u);
         if (!TAPS && wide_of<Map>(P)) {
             const float4 nd = P.hitn[i];
