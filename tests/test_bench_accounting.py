@@ -1,0 +1,65 @@
+"""bench.py's algorithmic accounting, host side: the per-kernel
+flop split covers the whole pipeline exactly once, and the pipeline-bytes
+model adds up.  Counters from the oracle's instrumented render of a small
+C3 frame (the same events the GPU's stats kernels count)."""
+import numpy as np
+import pytest
+
+import bench
+from compute_path_tracer_amd import scenes
+from compute_path_tracer_amd.sdf_editor import CompData
+from oracle import oracle as O
+
+
+@pytest.fixture(scope="module")
+def counters():
+    ed = scenes.c3_graph32()
+    prog = ed.compile(CompData())
+    w, h = 48, 32
+    _, ct = O.OracleScene(ed.rows()).render(w, h, O.Constants(0.0, 1, float(np.float32(w) / np.float32(h)), 1),
+                                            O.Settings(0, 8, 1.0, 1.0, 0), 2, counters=True)
+    return prog, ct, w * h
+
+
+def _taps_share(ct: dict) -> dict:
+    """A stand-in for the stats run's shade-pass tap half: every calc_normal
+    map() of the oracle (the counters split it out on the GPU)."""
+    taps = {k: 0 for k in ct}
+    taps["normal_maps"] = ct["normal_maps"]
+    return taps
+
+
+@pytest.mark.parametrize("gen_trace", [True, False])
+def test_flop_split_covers_the_pipeline_once(counters, gen_trace):
+    prog, ct, _ = counters
+    st = dict(ct, wave_maps=0, wave_shapes=0)
+    taps = _taps_share(ct)
+    total = bench.algorithmic_flops(st)
+    trace = bench.trace_flops(st, taps, prog.n_aabb, gen_trace)
+    shade = bench.shade_flops(st, taps, prog.n_aabb)
+    gen = 0.0 if gen_trace else (bench.W_CAMERA + bench.W_AABB * prog.n_aabb) * st["samples"]
+    fold = bench.W_ACCUM * st["samples"]
+    assert trace > 0 and shade > 0
+    assert trace + shade + gen + fold == pytest.approx(total, rel=0, abs=1e-3)
+    # the primary rays' bounds() are never the shade pass's: one test per box
+    # of each primary segment
+    assert st["aabb_tests"] >= st["samples"] * prog.n_aabb
+    if gen_trace:  # the first trace pass carries the camera rays and primary bounds()
+        assert trace - bench.trace_flops(st, taps, prog.n_aabb, False) == pytest.approx(
+            (bench.W_CAMERA + bench.W_AABB * prog.n_aabb) * st["samples"])
+
+
+def test_pipeline_bytes_add_up(counters):
+    _, ct, pixels = counters
+    for gen_trace in (True, False):
+        parts = bench.pipeline_bytes(ct, pixels, gen_trace=gen_trace)
+        assert parts["total"] == pytest.approx(sum(v for k, v in parts.items() if k != "total"))
+        assert parts["fold"] == 16.0 * ct["samples"] + 32.0 * pixels
+
+
+def test_hw_view_and_cpu_info():
+    hw = bench.hw_view({"valu_issue_frac_of_peak": 0.5, "valu_lane_utilization": 0.8, "salu_per_valu": 0.3})
+    assert hw["valu_lane_slots_busy"] == pytest.approx(0.4)
+    info = bench.cpu_info()
+    assert info["os_cpu_count"] >= 1 and info["affinity"] >= 1 and info["model"]
+    assert 1 <= bench.default_cpu_threads() <= info["affinity"]
