@@ -843,7 +843,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 map_point(TAPS ? state : int(ST_MARCH), step, ro, rd, t, qx, qy, qz);
                 uint64_t live = 0;  // (the taps' live mask: unused here)
                 const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, __builtin_inff(), __builtin_inff(), live, st);
-#if defined(PT_EXP_VALUPAD) || defined(PT_EXP_SALUPAD)  // timing probes: N extra independent VALU / SALU per map
+#if defined(PT_EXP_VALUPAD) || defined(PT_EXP_SALUPAD) || defined(PT_EXP_NOPPAD)  // timing probes: N extra independent VALU / SALU / `s_nop 1` per map
                 {
 #ifdef PT_EXP_VALUPAD
                     float a0 = qx, a1 = qy, a2 = qz, a3 = t;
@@ -859,6 +859,10 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                     for (int k = 0; k < PT_EXP_SALUPAD / 2; ++k)
                         __asm__ volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1));
                     __asm__ volatile("" ::"s"(s0), "s"(s1));
+#endif
+#ifdef PT_EXP_NOPPAD
+#pragma unroll
+                    for (int k = 0; k < PT_EXP_NOPPAD; ++k) __asm__ volatile("s_nop 1");
 #endif
                 }
 #endif

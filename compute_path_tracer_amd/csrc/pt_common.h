@@ -155,8 +155,52 @@ __device__ __forceinline__ void xform(const PtNode &n, float &x, float &y, float
 // are +0) and sqrt(RN(m^2)) = m exactly (binary RN; checked for every
 // significand), so length(max(q, 0)) = m without the squares and the sqrt.
 // A wave takes that path when all its active lanes qualify.
+#if (defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)) && !defined(PT_NO_BARE_MINMAX)
+// max(x, 0), min(x, 0), max3 and med3 as the bare instructions.  fmaxf's
+// IEEE-mode lowering first quiets each operand produced in another basic
+// block (one `v_max_f32 v, v, v` each; the cube's q comes from before the
+// cull branch).  No operand here is a signalling NaN, and for the rest (quiet
+// NaN included: the other operand) the instructions return fmaxf's / fminf's
+// / fmed3's values.  PT_NO_BARE_MINMAX: the builtins (A/B).
+__device__ __forceinline__ float pt_max0(float x) {
+    float r;
+    __asm__("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ float pt_min0(float x) {
+    float r;
+    __asm__("v_min_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ float pt_max3v(float a, float b, float c) {
+    float r;
+    __asm__("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float pt_med3v(float a, float b, float c) {
+    float r;
+    __asm__("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+#define PT_BARE_MINMAX 1
+#else
+__device__ __forceinline__ float pt_max0(float x) { return pt_gmax(x, 0.0f); }
+__device__ __forceinline__ float pt_min0(float x) { return pt_gmin(x, 0.0f); }
+#endif
 template <bool FAST = false>
 __device__ __forceinline__ float cube_from_q(float qx, float qy, float qz, float qm) {
+#if defined(PT_BARE_MINMAX)
+    // (no bare instruction inside a branch: clang marks inline asm convergent,
+    // which kept the ballot's branch from folding into the compares)
+    const float mx = pt_max0(qx), my = pt_max0(qy), mz = pt_max0(qz), mq = pt_min0(qm);
+    if constexpr (FAST) {
+        const float m = pt_max3v(mx, my, mz);
+        const bool easy = pt_med3v(mx, my, mz) == 0.0f &&
+                          (m == 0.0f || __builtin_amdgcn_fmed3f(m, 0x1p-60f, 0x1p60f) == m);
+        if (__ballot(!easy) == 0ull) return m + mq;
+    }
+    return pt_sqrt(mx * mx + my * my + mz * mz) + mq;
+#else
     const float mx = pt_gmax(qx, 0.0f), my = pt_gmax(qy, 0.0f), mz = pt_gmax(qz, 0.0f);
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
     if constexpr (FAST) {
@@ -167,6 +211,7 @@ __device__ __forceinline__ float cube_from_q(float qx, float qy, float qz, float
     }
 #endif
     return pt_sqrt(mx * mx + my * my + mz * mz) + pt_gmin(qm, 0.0f);
+#endif
 }
 
 // cull target: the smaller of the parent's running distance a and the
