@@ -97,6 +97,7 @@ struct pt_ctx {
     size_t bin_cap = 0, ctrl_words = 0;
     hipStream_t xstream[kMaxLanes] = {};   // lanes 1.. streams (created on first use; lane 0 = stream)
     hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {};
+    std::vector<hipEvent_t> order_ev;      // PT_LANE_ORDER: one per (lane, pass) trace launch
     int bin_lanes = -1;                    // pt_set_option "bin_lanes"; -1 = env PT_BIN_LANES
     int shade_taps = -1;                   // pt_set_option "shade_taps"; -1 = env PT_SHADE_TAPS
     int gen_trace_used = 0;                // the last timed dispatch's first pass made its own camera rays
@@ -952,6 +953,24 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             if (!stats) HIPCHK(c, record_event(c->slog, c->lane[i].stream));
             return PT_OK;
         };
+        // A/B knob PT_LANE_ORDER: the lanes' trace launches ordered by events.
+        // 1: lane i's first trace pass starts after lane i-1's has ended
+        // (staggered start); 2: the trace passes alternate, lane i's pass k
+        // after lane i-1's pass k and lane 0's pass k after the last lane's
+        // pass k-1 (a lane's shade and scatter run beside the next lane's trace)
+        static const int lane_order = [] {
+            const char *v = std::getenv("PT_LANE_ORDER");
+            return v ? std::atoi(v) : 0;
+        }();
+        const bool ordered = lane_order != 0 && nl > 1;
+        if (ordered) {
+            while (c->order_ev.size() < size_t(nl) * size_t(passes)) {
+                hipEvent_t e;
+                HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                c->order_ev.push_back(e);
+            }
+        }
+        auto order_ev = [&](int i, int k) { return c->order_ev[size_t(k) * size_t(nl) + size_t(i)]; };
         for (int k = 0; k < passes; ++k) {
             for (int i = 0; i < nl; ++i) {
                 // pass k: bin the rays of ray[k & 1] (gen's, or the shaded hits of pass k-1), trace them into the other
@@ -971,6 +990,12 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                                   l.stream);
                     HIPCHK(c, hipGetLastError());
                 }
+                if (ordered) {
+                    if (lane_order == 1 && k == 0 && i > 0)
+                        HIPCHK(c, hipStreamWaitEvent(l.stream, order_ev(i - 1, 0), 0));
+                    else if (lane_order == 2 && (i > 0 || k > 0))
+                        HIPCHK(c, hipStreamWaitEvent(l.stream, i > 0 ? order_ev(i - 1, k) : order_ev(nl - 1, k - 1), 0));
+                }
                 if (!stats) HIPCHK(c, record_event(c->tlog, l.stream));
                 if (jit) {
                     void *args[] = {&p};
@@ -981,6 +1006,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                     HIPCHK(c, hipGetLastError());
                 }
                 if (!stats) HIPCHK(c, record_event(c->tlog, l.stream));
+                if (ordered) HIPCHK(c, hipEventRecord(order_ev(i, k), l.stream));
             }
         }
         for (int i = 0; i < nl; ++i)  // the last bounce's hits end their paths
@@ -1347,6 +1373,7 @@ void pt_destroy(pt_ctx *c) {
         if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
     }
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    for (hipEvent_t e : c->order_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (hipEvent_t e : c->tlog.ev) (void)hipEventDestroy(e);
