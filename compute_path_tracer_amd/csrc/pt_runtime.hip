@@ -812,11 +812,10 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     if (trace_cu_env > 0 && trace_cu_env < per_cu) per_cu = trace_cu_env;
     // default: leave one wave slot per SIMD (4 per CU) to the other pipeline,
     // so its shade / scatter / scan blocks run beside the persistent trace
-    // waves instead of waiting for a pass to drain (24 of 28: +1.5 %)
-    else if (trace_cu_env == 0 && per_cu > 8) per_cu = std::min(per_cu - 4, 24);
-    // (at most 6 per SIMD: with the 64-VGPR narrow-scene kernel, 7 left the
-    // other pipeline's one-wave scan waiting ~1.7 ms per pass; 24 vs 28:
-    // +1.5 %)
+    // waves instead of waiting for a pass to drain: 28 of 32 with the 64-VGPR
+    // (8-wave) build (+1.5 % over 24 of 28 at 72 VGPRs), 24 of 28 with the
+    // 72-VGPR fallback (+1.5 % over 28 of 28)
+    else if (trace_cu_env == 0 && per_cu > 8) per_cu = std::min(per_cu - 4, 28);
     const unsigned trace_grid = cu * unsigned(std::max(1, per_cu));
     static const int run_max = [] {  // A/B knob
         const char *v = std::getenv("PT_BIN_RUN");
