@@ -255,3 +255,33 @@ def test_run_cut_carries_the_underflow_guard(tmp_path):
     assert all(g for g in runs), runs
     assert not re.search(r"if \(!?\(?qm > h\d+\.d\)", src)
     assert all("qm > 0x1p-60f" in m for m in re.findall(r"const bool cut_q = [^;]*;", src))
+
+
+def _compile_log(scene: str) -> str:
+    prog = scenes.SCENES[scene]().compile(CompData())
+    old = os.environ.get("PT_JIT_BAKE")
+    os.environ["PT_JIT_BAKE"] = "1"
+    try:
+        log = ctypes.create_string_buffer(1 << 16)
+        rc = N.lib().pt_jit_compile(prog.ops, prog.n_ops, prog.aabbs, prog.n_aabb,
+                                    prog.data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(prog.data), log,
+                                    len(log), None)
+    finally:
+        if old is None:
+            os.environ.pop("PT_JIT_BAKE", None)
+        else:
+            os.environ["PT_JIT_BAKE"] = old
+    assert rc == N.PT_OK, log.value.decode()
+    return log.value.decode(errors="replace")
+
+
+@pytest.mark.parametrize("scene,fallback", [("c3", False), ("wide", True)])
+def test_spilling_build_falls_back_to_seven_waves(scene, fallback, tmp_path):
+    """The scene kernels are built for 8 waves per SIMD (64 VGPRs); a build
+    whose trace kernels spill, or whose shade kernel spills more than 16 bytes
+    per lane, is rebuilt at 7 (pt_jit.cpp pt_jit_compile_source).  C3 keeps
+    the 8-wave build; the 128-entry `wide` scene spills and falls back."""
+    src, _ = _baked(scene, tmp_path)
+    assert "#define PT_TW_N 8" in src and "#define PT_SW_N 8" in src
+    assert "amdgpu_waves_per_eu(PT_TW_N)" in src
+    assert _compile_log(scene).startswith("(rebuilt at 7 waves per SIMD") == fallback
