@@ -305,6 +305,13 @@ __device__ __forceinline__ void bin_scan_fused(const PtPass &P, uint32_t *lds) {
 // together, and the per-hit map() bound (pt_path.h tap_bound, from the hit
 // record) lets each tap drop every shape that provably lies farther away
 // (DESIGN.md 3.13).
+// PT_SHADE_EARLY=1 (A/B, default 0): the shade pass decides early ends
+// before the taps and compacts the rest (bin_shade_body).  Measured equal
+// alone (68.9 vs 68.6 ms per step) and −1.5 % with two pipelines: the second
+// load of each queued record costs what the skipped taps and slab tests save
+#ifndef PT_SHADE_EARLY
+#define PT_SHADE_EARLY 0
+#endif
 template <class Map, bool ST, bool TAPS>
 __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
@@ -430,6 +437,83 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         P.key[i] = k;
         atomicAdd(&lh[k], 1u);
     };
+#if PT_SHADE_EARLY
+    // Early ends (timed kernel; the instrumented one keeps the reference's
+    // work: every hit taps, as the oracle counts it).  Whether a hit's path
+    // ends here -- Russian roulette, the bounce limit -- and its emission do
+    // not depend on the normal (shade_lane: the draws, the throughput update
+    // and the roulette use only the record's throughput, rng and material),
+    // so each wave first decides that for 64 positions from two of the
+    // record's four words, finishes the ending paths (colour slot, no bin)
+    // and queues the others in LDS; full waves of those then tap, shade and
+    // take bounds(): the ~30 % of hits that end (C3) no longer idle through
+    // the taps and the slab tests.
+    if constexpr (!ST) {
+        __shared__ uint32_t sq[PT_BIN_BLOCK / 64][128];  // per wave: a ring of queued positions
+        const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+        uint32_t qh = 0u, qn = 0u;  // (wave-uniform)
+        auto run = [&](uint32_t cnt) {
+            if (ln < cnt) {
+                const uint32_t j = sq[wv][(qh + ln) & 127u];
+                const uint4 q0 = P.rin[j].q[0], q1 = P.rin[j].q[1], q2 = P.rin[j].q[2], q3 = P.rin[j].q[3];
+                uint2 hi = make_uint2(0u, 0u);
+                if (!TAPS && wide_of<Map>(P)) {
+                    const float4 nd = P.hitn[j];
+                    hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
+                }
+                shade_one(j, q0, q1, q2, q3, hi);
+            }
+            qh += cnt;
+            qn -= cnt;
+        };
+        const uint32_t stride = gridDim.x * blockDim.x;
+        for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
+            const uint32_t i = base + ln;
+            bool queue = false;
+            if (i < n) {
+                const uint4 q1 = P.rin[i].q[1], q2 = P.rin[i].q[2];
+                if (q2.w == PT_AUX_MISS) {
+                    P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
+                } else {
+                    // shade_lane's own decision, with a stand-in normal (it
+                    // changes the next direction only) and no counters
+                    pt_f3 thr{__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
+                    pt_f3 ro{0.0f, 0.0f, 0.0f}, rd{0.0f, 0.0f, 1.0f}, ret{0.0f, 0.0f, 0.0f};
+                    uint32_t rng = q2.y;
+                    int seg = P.bounce;
+                    Stats<false> none;
+                    if (shade_lane<false>(mats, L.bounces, int(q2.w), 0.0f, 0.0f, 1.0f, 0, rng, ro, rd, thr, ret, seg,
+                                          none)) {
+                        const uint32_t sid = q2.z;
+                        if (P.gen_trace) {
+                            P.color[sid] = make_float4(ret.x, ret.y, ret.z, 0.0f);
+                        } else if (ret.x != 0.0f || ret.y != 0.0f || ret.z != 0.0f) {
+                            float4 c = P.color[sid];
+                            c.x += ret.x;
+                            c.y += ret.y;
+                            c.z += ret.z;
+                            P.color[sid] = c;
+                        }
+                        if (L.debug == 3) {
+                            const pt_f3 col = final_color(L.debug, seg, L.bounces, ret);
+                            P.color[sid] = make_float4(col.x, col.y, col.z, 0.0f);
+                        }
+                        P.key[i] = PT_BIN_NONE;
+                    } else {
+                        queue = true;
+                    }
+                }
+            }
+            const uint64_t qm = __ballot(queue);
+            if (queue) sq[wv][(qh + qn + uint32_t(lane_rank(qm))) & 127u] = i;
+            qn += uint32_t(__popcll(qm));
+            __builtin_amdgcn_wave_barrier();
+            if (qn >= 64u) run(64u);
+        }
+        if (qn > 0u) run(qn);
+    } else
+#endif
+    {
     // Nearly every position holds a hit (misses end in the trace pass), so
     // each thread takes one position and loads its whole record (a miss
     // marks its record's q2): one memory round trip.
@@ -455,6 +539,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         }
         if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
         else shade_one(i, q0, q1, q2, q3, hi);
+    }
     }
     hist_flush(lh, P.hist);
     if (P.scan_ctrl) bin_scan_fused(P, lh);
