@@ -1323,6 +1323,7 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "jit_tier_active")) *value = c->jit_tier.module ? 1.0 : 0.0;
     else if (!std::strcmp(key, "jit_tier_seconds")) *value = c->tier_seconds;
     else if (!std::strcmp(key, "jit_seconds")) *value = c->jit_seconds;
+    else if (!std::strcmp(key, "jit_isolated")) *value = pt_jit_isolated();
     else if (!std::strcmp(key, "kernel")) *value = c->kernel;
     else if (!std::strcmp(key, "shade_batch")) *value = c->shade_batch;
     else if (!std::strcmp(key, "bin_samples")) *value = double(bin_samples(c));
