@@ -545,7 +545,8 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
         "schedule": schedule_metrics(st, taps),
         "jit": {"active": jit, "compile_s": round(pt.get_option("jit_seconds"), 3),
                 "tier_active": bool(pt.get_option("jit_tier_active")),
-                "tier_compile_s": round(pt.get_option("jit_tier_seconds"), 3)},
+                "tier_compile_s": round(pt.get_option("jit_tier_seconds"), 3),
+                "compiler": "image hipRTC, own namespace" if pt.get_option("jit_isolated") == 1 else "process hipRTC"},
     }
     if shade is not None:
         out["roofline"]["shade"] = shade

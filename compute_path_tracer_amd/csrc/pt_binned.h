@@ -312,6 +312,9 @@ __device__ __forceinline__ void bin_scan_fused(const PtPass &P, uint32_t *lds) {
 #ifndef PT_SHADE_EARLY
 #define PT_SHADE_EARLY 0
 #endif
+#ifndef PT_SHADE_GROUP
+#define PT_SHADE_GROUP 0
+#endif
 template <class Map, bool ST, bool TAPS>
 __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
@@ -511,6 +514,59 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             if (qn >= 64u) run(64u);
         }
         if (qn > 0u) run(qn);
+    } else
+#endif
+#if PT_SHADE_GROUP
+    // Hits grouped by what they hit (timed kernel, A/B): a wave's normal taps
+    // evaluate every shape any of its lanes keeps live, and the hits of a
+    // wave lie on different shapes (2.3 evaluations per tap where a lane
+    // needs 1.1).  Each block takes its 256 positions in material order (the
+    // material is the shape's index, record q2.w): an LDS counting sort of the
+    // chunk's keys, which were loaded one chunk ahead so the sort waits on no
+    // load; misses sort last.  Outputs still go to each record's own position.
+    if constexpr (!ST && NM > 0 && NM < 63) {
+        __shared__ uint32_t gcnt[64];
+        __shared__ unsigned short gperm[PT_BIN_BLOCK];
+        const uint32_t t = threadIdx.x;
+        const uint32_t stride = gridDim.x * blockDim.x;
+        auto key_of = [&](uint32_t i) -> uint32_t {
+            if (i >= n) return 63u;
+            const uint32_t m = P.rin[i].q[2].w;  // material, or PT_AUX_MISS
+            return m < uint32_t(NM) ? m : uint32_t(NM);
+        };
+        uint32_t base = blockIdx.x * blockDim.x;
+        uint32_t mk = key_of(base + t);
+        for (; base < n; base += stride) {  // (block-uniform)
+            if (t < 64u) gcnt[t] = 0u;
+            __syncthreads();
+            const uint32_t rank = atomicAdd(&gcnt[mk], 1u);
+            __syncthreads();
+            if (t < 64u) {  // exclusive prefix of the 64 counts (wave 0)
+                const uint32_t c = gcnt[t];
+                uint32_t inc = c;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t x = uint32_t(__shfl_up(int(inc), off, 64));
+                    if (t >= uint32_t(off)) inc += x;
+                }
+                gcnt[t] = inc - c;
+            }
+            __syncthreads();
+            gperm[gcnt[mk] + rank] = (unsigned short)t;
+            __syncthreads();
+            const uint32_t i = base + gperm[t];
+            mk = key_of(base + stride + t);  // the next chunk's key, one chunk ahead
+            if (i < n) {
+                const uint4 q0 = P.rin[i].q[0], q1 = P.rin[i].q[1], q2 = P.rin[i].q[2], q3 = P.rin[i].q[3];
+                uint2 hi = make_uint2(0u, 0u);
+                if (!TAPS && wide_of<Map>(P)) {
+                    const float4 nd = P.hitn[i];
+                    hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
+                }
+                if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;
+                else shade_one(i, q0, q1, q2, q3, hi);
+            }
+        }
     } else
 #endif
     {
