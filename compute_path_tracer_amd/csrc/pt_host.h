@@ -50,9 +50,6 @@ std::string pt_jit_source(const std::vector<PtNode> &nodes, const std::vector<Pt
                           bool bake);
 // Compile with hipRTC for gfx950; returns the code object or an error log.
 bool pt_jit_compile_source(const std::string &src, std::vector<char> &code, std::string &log);
-// 1: hipRTC came from this image's ROCm in its own link-map namespace, 0: the
-// process's default one (pt_jit.cpp hiprtc()), -1: none found
-int pt_jit_isolated();
 // Load a code object on the current device.
 bool pt_jit_load(const std::vector<char> &code, PtJitModule &m, std::string &err);
 void pt_jit_unload(PtJitModule &m);

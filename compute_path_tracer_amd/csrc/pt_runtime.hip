@@ -1323,7 +1323,15 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "jit_tier_active")) *value = c->jit_tier.module ? 1.0 : 0.0;
     else if (!std::strcmp(key, "jit_tier_seconds")) *value = c->tier_seconds;
     else if (!std::strcmp(key, "jit_seconds")) *value = c->jit_seconds;
-    else if (!std::strcmp(key, "jit_isolated")) *value = pt_jit_isolated();
+    else if (!std::strcmp(key, "jit_trace_vgprs") || !std::strcmp(key, "jit_shade_vgprs")) {
+        // registers of the scene kernel in use: 64 = the 8-wave build, 72 = the
+        // 7-wave rebuild after a spill (pt_jit_compile_source); 0 = none
+        const PtJitModule *m = jit_active(c);
+        const hipFunction_t f = m ? (key[4] == 't' ? m->trace_m : m->shade_t) : nullptr;
+        int regs = 0;
+        if (f && hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, f) != hipSuccess) regs = 0;
+        *value = regs;
+    }
     else if (!std::strcmp(key, "kernel")) *value = c->kernel;
     else if (!std::strcmp(key, "shade_batch")) *value = c->shade_batch;
     else if (!std::strcmp(key, "bin_samples")) *value = double(bin_samples(c));

@@ -284,38 +284,14 @@ def test_spilling_build_falls_back_to_seven_waves(scene, fallback, tmp_path):
     src, _ = _baked(scene, tmp_path)
     assert "#define PT_TW_N 8" in src and "#define PT_SW_N 8" in src
     assert "amdgpu_waves_per_eu(PT_TW_N)" in src
-    log = _compile_log(scene)
-    spills = [ln.strip() for ln in log.splitlines() if "Function Name" in ln or "ScratchSize" in ln]
-    assert log.startswith("(rebuilt at 7 waves per SIMD") == fallback, "\n".join(spills)
-
-
-def test_scene_kernels_use_the_images_compiler_after_torch():
-    """PyTorch bundles an older libhiprtc / libamd_comgr; a process that
-    imports torch before the first scene compile (every GPU test, bench.py
-    at N > 1) used to compile with them, and their register allocation made
-    C3's 8-wave build spill and fall back to 7 waves.  pt_jit.cpp loads this
-    image's hipRTC into a link-map namespace of its own (dlmopen), so the
-    build no longer depends on import order."""
+    # (in a fresh process: one that imported torch first compiles with torch's
+    # bundled hipRTC / comgr, whose allocation spills C3 at 8 waves -- DESIGN.md 5)
     import subprocess
     import sys
 
-    prog = r"""
-import ctypes, os, sys
-import torch  # noqa: F401 -- loads torch's bundled hipRTC / comgr first
-sys.path.insert(0, sys.argv[1])
-os.environ["PT_JIT_BAKE"] = "1"
-from compute_path_tracer_amd import _native as N, scenes
-from compute_path_tracer_amd.sdf_editor import CompData
-p = scenes.SCENES["c3"]().compile(CompData())
-log = ctypes.create_string_buffer(1 << 16)
-rc = N.lib().pt_jit_compile(p.ops, p.n_ops, p.aabbs, p.n_aabb,
-                            p.data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(p.data), log, len(log), None)
-maps = open("/proc/self/maps").read()
-print(rc, int(log.value.startswith(b"(rebuilt")), int("torch/lib/libhiprtc" in maps))
-"""
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = subprocess.run([sys.executable, "-c", prog, root], capture_output=True, text=True, timeout=600)
+    prog = (f"import sys; sys.path.insert(0, {os.path.dirname(os.path.abspath(__file__))!r}); "
+            f"import test_cull as T; print(T._compile_log({scene!r}).splitlines()[0])")
+    out = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, out.stderr[-2000:]
-    rc, rebuilt, torch_rtc = out.stdout.split()[-3:]
-    assert rc == "0" and torch_rtc == "1"  # (torch's copy is loaded, yet not used)
-    assert rebuilt == "0", "C3's scene kernels fell back to 7 waves after importing torch"
+    assert out.stdout.startswith("(rebuilt at 7 waves per SIMD") == fallback, out.stdout[:500]
+
