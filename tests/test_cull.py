@@ -295,3 +295,61 @@ def test_spilling_build_falls_back_to_seven_waves(scene, fallback, tmp_path):
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.startswith("(rebuilt at 7 waves per SIMD") == fallback, out.stdout[:500]
 
+
+
+_PROBE = r"""
+import ctypes, os, sys
+if sys.argv[2] == "torch":
+    import torch  # noqa: F401 -- torch's bundled hipRTC / comgr are loaded first
+sys.path.insert(0, sys.argv[1])
+from compute_path_tracer_amd import _native as N, scenes
+from compute_path_tracer_amd.sdf_editor import CompData
+os.environ["PT_JIT_BAKE"] = sys.argv[4]
+p = scenes.SCENES[sys.argv[3]]().compile(CompData())
+log = ctypes.create_string_buffer(1 << 16)
+size = ctypes.c_size_t()
+rc = N.lib().pt_jit_compile(p.ops, p.n_ops, p.aabbs, p.n_aabb, p.data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                            len(p.data), log, len(log), ctypes.byref(size))
+print(rc, int(log.value.startswith(b"(rebuilt")), size.value)
+"""
+
+
+def _probe(scene: str, bake: str, first: str = "none", **env):
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if not k.startswith("PT_JIT")}
+    e.update(env)
+    out = subprocess.run([sys.executable, "-c", _PROBE, root, first, scene, bake], capture_output=True, text=True,
+                         timeout=900, env=e)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rc, rebuilt, size = out.stdout.split()[-3:]
+    assert rc == "0"
+    return rebuilt == "1", int(size)
+
+
+def test_jit_disk_cache_round_trip(tmp_path):
+    """pt_jit.cpp's on-disk cache: PT_JIT_CACHE=2 writes one entry per
+    generated source, a later process reads the same code object back, and a
+    compile knob that changes the build changes the key (a miss)."""
+    d = str(tmp_path)
+    _, size = _probe("c1", "1", PT_JIT_CACHE="2", PT_JIT_CACHE_DIR=d)
+    files = sorted(os.listdir(d))
+    assert len(files) == 1 and files[0].endswith(".ptjit")
+    with open(os.path.join(d, files[0]), "rb") as f:
+        assert f.read(8) == b"PTJIT1\0\0"
+    assert _probe("c1", "1", PT_JIT_CACHE="1", PT_JIT_CACHE_DIR=d)[1] == size
+    _probe("c1", "1", PT_JIT_CACHE="2", PT_JIT_CACHE_DIR=d, PT_JIT_SHADE_SPILL_OK="17")
+    assert len(os.listdir(d)) == 2
+
+
+def test_shipped_scene_kernels_survive_a_torch_first_process():
+    """A process that imported torch first holds torch's bundled, older
+    hipRTC, whose register allocation makes C3's 8-wave build spill (the 7-wave
+    rebuild runs 4-5 % slower).  build() ships the BASELINE
+    scenes' kernels in lib/jitcache, compiled with this image's hipRTC, so that
+    process still loads the 8-wave build; with the cache off it does not."""
+    assert _probe("c3", "1", first="torch") == _probe("c3", "1", first="none")
+    assert _probe("c3", "1", first="torch")[0] is False
+    assert _probe("c3", "1", first="torch", PT_JIT_CACHE="0")[0] is True
