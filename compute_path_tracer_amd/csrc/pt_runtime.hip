@@ -817,6 +817,15 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     // 72-VGPR fallback (+1.5 % over 28 of 28)
     else if (trace_cu_env == 0 && per_cu > 8) per_cu = std::min(per_cu - 4, 28);
     const unsigned trace_grid = cu * unsigned(std::max(1, per_cu));
+    // the first pass's kernel may have been rebuilt at 7 waves on its own
+    // (pt_jit_compile_source): the same one-slot-per-SIMD rule on its occupancy
+    unsigned trace_g_grid = trace_grid;
+    if (jit && jm->trace_g && trace_cu_env == 0) {
+        int g = 0;
+        HIPCHK(c, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&g, jm->trace_g, 64, 0));
+        if (g > 8) g = std::min(g - 4, 28);
+        if (g > 0 && g < per_cu) trace_g_grid = cu * unsigned(g);
+    }
     static const int run_max = [] {  // A/B knob
         const char *v = std::getenv("PT_BIN_RUN");
         const int r = v ? std::atoi(v) : 512;
@@ -998,7 +1007,8 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 if (!stats) HIPCHK(c, record_event(c->tlog, l.stream));
                 if (jit) {
                     void *args[] = {&p};
-                    HIPCHK(c, hipModuleLaunchKernel(gt ? jm->trace_g : jf, trace_grid, 1, 1, 64, 1, 1, 0, l.stream, args,
+                    HIPCHK(c, hipModuleLaunchKernel(gt ? jm->trace_g : jf, gt ? trace_g_grid : trace_grid, 1, 1, 64, 1,
+                                                    1, 0, l.stream, args,
                                                     nullptr));
                 } else {
                     pt_launch_bin(PtBinStage::Trace, p, stats, trace_grid, l.stream);
