@@ -337,8 +337,14 @@ def test_jit_disk_cache_round_trip(tmp_path):
     _, size = _probe("c1", "1", PT_JIT_CACHE="2", PT_JIT_CACHE_DIR=d)
     files = sorted(os.listdir(d))
     assert len(files) == 1 and files[0].endswith(".ptjit")
-    with open(os.path.join(d, files[0]), "rb") as f:
-        assert f.read(8) == b"PTJIT1\0\0"
+    path = os.path.join(d, files[0])
+    with open(path, "rb") as f:
+        assert f.read(8) == b"PTJIT2\0\0"
+    assert _probe("c1", "1", PT_JIT_CACHE="1", PT_JIT_CACHE_DIR=d)[1] == size
+    # a damaged entry is a miss (checksum), not a broken kernel: the scene compiles
+    with open(path, "r+b") as f:
+        f.seek(-100, 2)
+        f.write(b"\xff" * 8)
     assert _probe("c1", "1", PT_JIT_CACHE="1", PT_JIT_CACHE_DIR=d)[1] == size
     _probe("c1", "1", PT_JIT_CACHE="2", PT_JIT_CACHE_DIR=d, PT_JIT_SHADE_SPILL_OK="17")
     assert len(os.listdir(d)) == 2
