@@ -546,8 +546,8 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
         "jit": {"active": jit, "compile_s": round(pt.get_option("jit_seconds"), 3),
                 "tier_active": bool(pt.get_option("jit_tier_active")),
                 "tier_compile_s": round(pt.get_option("jit_tier_seconds"), 3),
-                "trace_vgprs": int(pt.get_option("jit_trace_vgprs")),
-                "shade_vgprs": int(pt.get_option("jit_shade_vgprs"))},
+                "trace_waves_per_simd": pt.get_option("jit_trace_waves"),
+                "shade_waves_per_simd": pt.get_option("jit_shade_waves")},
     }
     if shade is not None:
         out["roofline"]["shade"] = shade

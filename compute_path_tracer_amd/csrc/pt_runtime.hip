@@ -1333,14 +1333,16 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "jit_tier_active")) *value = c->jit_tier.module ? 1.0 : 0.0;
     else if (!std::strcmp(key, "jit_tier_seconds")) *value = c->tier_seconds;
     else if (!std::strcmp(key, "jit_seconds")) *value = c->jit_seconds;
-    else if (!std::strcmp(key, "jit_trace_vgprs") || !std::strcmp(key, "jit_shade_vgprs")) {
-        // registers of the scene kernel in use: 64 = the 8-wave build, 72 = the
-        // 7-wave rebuild after a spill (pt_jit_compile_source); 0 = none
+    else if (!std::strcmp(key, "jit_trace_waves") || !std::strcmp(key, "jit_shade_waves")) {
+        // waves per SIMD the scene kernel in use can hold: 8 = the 8-wave build
+        // (<= 64 VGPRs), 7 = the rebuild after a spill (pt_jit_compile_source)
         const PtJitModule *m = jit_active(c);
-        const hipFunction_t f = m ? (key[4] == 't' ? m->trace_m : m->shade_t) : nullptr;
-        int regs = 0;
-        if (f && hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, f) != hipSuccess) regs = 0;
-        *value = regs;
+        const bool tr = key[4] == 't';
+        const hipFunction_t f = m ? (tr ? m->trace_m : m->shade_t) : nullptr;
+        const int threads = tr ? 64 : PT_BIN_BLOCK;
+        int blocks = 0;
+        if (f && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, threads, 0) != hipSuccess) blocks = 0;
+        *value = double(blocks) * (threads / 64) / 4.0;  // (4 SIMDs per CU)
     }
     else if (!std::strcmp(key, "kernel")) *value = c->kernel;
     else if (!std::strcmp(key, "shade_batch")) *value = c->shade_batch;

@@ -457,7 +457,7 @@ def test_shipped_scene_kernels_in_a_torch_process(gpu, name):
     """This process imported torch before the library (conftest's GPU probe),
     so it holds torch's bundled hipRTC; the BASELINE scenes' kernels still
     come from lib/jitcache, built by build() with this image's hipRTC
-    (DESIGN.md 5): the 8-wave build (64 VGPRs) runs, for the table kernel and
+    (DESIGN.md 5): the 8-wave build runs, for the table kernel and
     the values-baked tier-up alike, and renders the oracle's image."""
     import sys
 
@@ -466,11 +466,11 @@ def test_shipped_scene_kernels_in_a_torch_process(gpu, name):
     prog = ed.compile(CompData())
     st = N.Settings(debug=0, bounces=3, scale=1.0, fov=1.0, aabb=0)
     pt = PathTracer(48, 32, prog, settings=st, options={"kernel": "binned", "jit": 1, "jit_bake": 2})
-    assert pt.get_option("jit_trace_vgprs") == 64 and pt.get_option("jit_shade_vgprs") == 64
+    assert pt.get_option("jit_trace_waves") == 8 and pt.get_option("jit_shade_waves") == 8
     assert pt.get_option("jit_seconds") < 1.0  # (a cache hit, not a 5-25 s compile)
     pt.set_option("jit_wait", 1)
     assert pt.get_option("jit_tier_active") == 1.0
-    assert pt.get_option("jit_trace_vgprs") == 64 and pt.get_option("jit_shade_vgprs") == 64
+    assert pt.get_option("jit_trace_waves") == 8 and pt.get_option("jit_shade_waves") == 8
     a = float(np.float32(48) / np.float32(32))
     pt.dispatch(N.Constants(time=0.0, frame=1, aspect=a, last_clear=1), 2)
     gpu_img = pt.read_image()
