@@ -315,6 +315,9 @@ __device__ __forceinline__ void bin_scan_fused(const PtPass &P, uint32_t *lds) {
 #ifndef PT_SHADE_GROUP
 #define PT_SHADE_GROUP 0
 #endif
+#ifndef PT_SHADE_PIPE
+#define PT_SHADE_PIPE 0
+#endif
 template <class Map, bool ST, bool TAPS>
 __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
@@ -337,8 +340,11 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     stt.init();
     const PtLaunch &L = P.L;
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
+    // `before_stores`: called once the colour slot is updated and the next
+    // segment's bounds() mask is known, before the position's key / next-ray
+    // stores (PT_SHADE_PIPE issues the next record's loads there)
     auto shade_one = [&](uint32_t i, const uint4 &q0, const uint4 &q1, const uint4 &q2, const uint4 &q3,
-                         const uint2 &hi) {
+                         const uint2 &hi, auto &&before_stores) {
         pt_f3 ro{__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
         pt_f3 rd{__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
         pt_f3 thr{__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
@@ -417,6 +423,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             P.color[sid] = c;
         }
         if (done) {
+            before_stores();
             if (L.debug == 3) {  // bounce-count view: the colour is the segment count, not the radiance
                 const pt_f3 col = final_color(L.debug, seg, L.bounces, ret);
                 P.color[sid] = make_float4(col.x, col.y, col.z, 0.0f);
@@ -434,6 +441,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             m.y |= m2.y;
         }
 #endif
+        before_stores();
         store_ray(P.rin + i, ro, rd, thr, rng, sid, 0u, make_uint4(m.x, m.y, 0u, 0u));
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);
@@ -464,7 +472,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                     const float4 nd = P.hitn[j];
                     hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
                 }
-                shade_one(j, q0, q1, q2, q3, hi);
+                shade_one(j, q0, q1, q2, q3, hi, [] {});
             }
             qh += cnt;
             qn -= cnt;
@@ -516,6 +524,45 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         if (qn > 0u) run(qn);
     } else
 #endif
+#if PT_SHADE_PIPE
+    // (A/B) The next position's record loads issued after this position's
+    // colour update and before its key / next-ray stores.  gfx950 has one
+    // vmcnt for loads and stores, retired in order, so a record load issued
+    // behind the previous position's stores (the default loop) waits for
+    // those stores to complete as well; issued ahead of them it does not.
+    // The record is loaded once the shading is done, so it does not stay live
+    // through the taps (PT_SHADE_PREFETCH held it there and spilled).
+    if constexpr (!ST) {
+        const uint32_t stride = gridDim.x * blockDim.x;
+        uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+        uint4 q0 = make_uint4(0u, 0u, 0u, 0u), q1 = q0, q2 = q0, q3 = q0;
+        uint2 hi = make_uint2(0u, 0u);
+        auto load = [&](uint32_t j, uint4 &a, uint4 &b, uint4 &c, uint4 &d, uint2 &h) {
+            a = P.rin[j].q[0], b = P.rin[j].q[1], c = P.rin[j].q[2], d = P.rin[j].q[3];
+            if (!TAPS && wide_of<Map>(P)) {
+                const float4 nd = P.hitn[j];
+                h = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
+            }
+        };
+        if (i < n) load(i, q0, q1, q2, q3, hi);
+        while (i < n) {
+            const uint32_t in = i + stride;
+            uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0, n2 = n0, n3 = n0;
+            uint2 nh = make_uint2(0u, 0u);
+            auto pre = [&] {
+                if (in < n) load(in, n0, n1, n2, n3, nh);
+            };
+            if (q2.w == PT_AUX_MISS) {
+                pre();
+                P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
+            } else {
+                shade_one(i, q0, q1, q2, q3, hi, pre);
+            }
+            q0 = n0, q1 = n1, q2 = n2, q3 = n3, hi = nh;
+            i = in;
+        }
+    } else
+#endif
 #if PT_SHADE_GROUP
     // Hits grouped by what they hit (timed kernel, A/B): a wave's normal taps
     // evaluate every shape any of its lanes keeps live, and the hits of a
@@ -564,7 +611,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                     hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
                 }
                 if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;
-                else shade_one(i, q0, q1, q2, q3, hi);
+                else shade_one(i, q0, q1, q2, q3, hi, [] {});
             }
         }
     } else
@@ -594,7 +641,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
         }
         if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
-        else shade_one(i, q0, q1, q2, q3, hi);
+        else shade_one(i, q0, q1, q2, q3, hi, [] {});
     }
     }
     hist_flush(lh, P.hist);
