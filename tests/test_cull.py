@@ -289,7 +289,8 @@ def test_spilling_build_falls_back_to_seven_waves(scene, fallback, tmp_path):
     import subprocess
     import sys
 
-    prog = (f"import sys; sys.path.insert(0, {os.path.dirname(os.path.abspath(__file__))!r}); "
+    here = os.path.dirname(os.path.abspath(__file__))
+    prog = (f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; "
             f"import test_cull as T; print(T._compile_log({scene!r}).splitlines()[0])")
     out = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, out.stderr[-2000:]
