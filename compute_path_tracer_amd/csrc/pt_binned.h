@@ -318,6 +318,9 @@ __device__ __forceinline__ void bin_scan_fused(const PtPass &P, uint32_t *lds) {
 #ifndef PT_SHADE_PIPE
 #define PT_SHADE_PIPE 0
 #endif
+#ifndef PT_PARK_EARLY
+#define PT_PARK_EARLY 0
+#endif
 template <class Map, bool ST, bool TAPS>
 __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
@@ -920,6 +923,38 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         }
     };
 
+    // park the staged window in LDS (waits for its loads) and form the
+    // wave's check[] union (Check.alo/ahi) for the scene kernels: the masks of
+    // the lanes still mapping and of the whole window, so it also covers every
+    // lane this window's refills start
+    auto park = [&]() {
+        const bool mapping_now = state == ST_MARCH || (TAPS && state == ST_NORMAL);
+        const bool in_win = uint32_t(lane) < wcnt;
+        ck.alo = wave_or_u64((mapping_now ? ck.lo : 0ull) |
+                             (in_win ? (uint64_t(s3.x) | (uint64_t(s3.y) << 32)) : 0ull));
+#ifdef PT_JIT_AAND_ON
+        // and the bits all of them share: AND = ~OR(~m) (lanes outside add 0)
+        ck.aand = ~wave_or_u64((mapping_now ? ~ck.lo : 0ull) |
+                               (in_win ? ~(uint64_t(s3.x) | (uint64_t(s3.y) << 32)) : 0ull));
+#endif
+        ck.ahi = wide_of<Map>(P) ? wave_or_u64((mapping_now ? ck.hi : 0ull) |
+                                      (in_win ? (uint64_t(sh.x) | (uint64_t(sh.y) << 32)) : 0ull))
+                        : 0ull;
+        W[0][lane] = make_uint4(__float_as_uint(s0.x), __float_as_uint(s0.y), __float_as_uint(s0.z),
+                                __float_as_uint(s0.w));
+        W[1][lane] = make_uint4(__float_as_uint(s1.x), __float_as_uint(s1.y), __float_as_uint(s1.z),
+                                __float_as_uint(s1.w));
+        W[2][lane] = make_uint4(__float_as_uint(s2.x), __float_as_uint(s2.y), __float_as_uint(s2.z),
+                                __float_as_uint(s2.w));
+        W[3][lane] = s3;
+        if constexpr (MapWide<Map>::v != 0)
+            if (wide_of<Map>(P)) W[4][lane] = make_uint4(sh.x, sh.y, 0u, 0u);
+        in_lds = true;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+
     for (;;) {
         uint64_t tm = st.clk();
 #ifdef PT_DEFER_STORE
@@ -940,36 +975,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             const int r = lane_rank(freem);
             const int src = int(wtake) + r;
             const bool got = state == ST_FREE && uint32_t(r) < take;
-            if (!in_lds) {  // first refill from this window: park it in LDS (waits for its loads)
-                // the wave's check[] union (Check.alo/ahi) for the scene kernels:
-                // the masks of the lanes still mapping and of the whole window,
-                // so it also covers every lane this window's refills start
-                const bool mapping_now = state == ST_MARCH || (TAPS && state == ST_NORMAL);
-                const bool in_win = uint32_t(lane) < wcnt;
-                ck.alo = wave_or_u64((mapping_now ? ck.lo : 0ull) |
-                                     (in_win ? (uint64_t(s3.x) | (uint64_t(s3.y) << 32)) : 0ull));
-#ifdef PT_JIT_AAND_ON
-                // and the bits all of them share: AND = ~OR(~m) (lanes outside add 0)
-                ck.aand = ~wave_or_u64((mapping_now ? ~ck.lo : 0ull) |
-                                       (in_win ? ~(uint64_t(s3.x) | (uint64_t(s3.y) << 32)) : 0ull));
-#endif
-                ck.ahi = wide_of<Map>(P) ? wave_or_u64((mapping_now ? ck.hi : 0ull) |
-                                              (in_win ? (uint64_t(sh.x) | (uint64_t(sh.y) << 32)) : 0ull))
-                                : 0ull;
-                W[0][lane] = make_uint4(__float_as_uint(s0.x), __float_as_uint(s0.y), __float_as_uint(s0.z),
-                                        __float_as_uint(s0.w));
-                W[1][lane] = make_uint4(__float_as_uint(s1.x), __float_as_uint(s1.y), __float_as_uint(s1.z),
-                                        __float_as_uint(s1.w));
-                W[2][lane] = make_uint4(__float_as_uint(s2.x), __float_as_uint(s2.y), __float_as_uint(s2.z),
-                                        __float_as_uint(s2.w));
-                W[3][lane] = s3;
-                if constexpr (MapWide<Map>::v != 0)
-                    if (wide_of<Map>(P)) W[4][lane] = make_uint4(sh.x, sh.y, 0u, 0u);
-                in_lds = true;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
+            if (!in_lds) park();  // first refill from this window
             float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f, b0 = 0.0f, b1 = 0.0f, b2 = 0.0f, b3 = 0.0f;
             float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
             uint32_t d0 = 0u, d1 = 0u, d2 = 0u, d3 = 0u, e0 = 0u, e1 = 0u;
@@ -1064,6 +1070,12 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             }
         }
         tm = st.lap(PT_ST_CYC_MAP, tm);
+#if PT_PARK_EARLY
+        // (A/B) park a freshly staged window right after the map step, before
+        // this iteration's hit-record stores: waiting for its loads then does
+        // not also wait for stores issued behind them (one in-order vmcnt)
+        if (!in_lds && wcnt != 0u) park();
+#endif
 
         // ---- 3. hand finished segments on: a miss ends the path (its
         // colour slot already holds its radiance), a hit goes to the shade
