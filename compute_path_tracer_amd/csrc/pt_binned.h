@@ -788,6 +788,13 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     // the staged window, once its loads have landed: [part][lane], so a
     // refill reads a ray with 4 ds_read_b128 instead of 16 cross-lane moves
     __shared__ uint4 W[MapWide<Map>::v == 0 ? 4 : 5][64];  // (W[4]: check[] bits 64..127)
+#if PT_PARK_EARLY >= 2
+    // the next window's slots, copied here when the current window is parked:
+    // staging then reads them from LDS (lgkmcnt) instead of waiting on their
+    // vector load with vmcnt(0), which also waits for every hit-record store
+    // issued since (one in-order counter for loads and stores)
+    __shared__ uint32_t WS[64];
+#endif
     const PtLaunch &L = P.L;
     const int lane = int(threadIdx.x);
     Stats<ST> st;
@@ -874,19 +881,28 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             s3 = make_uint4(m.x, m.y, 0u, 0u);
             sh = make_uint2(m.z, m.w);
         } else if (uint32_t(lane) < wcnt) {
-            const uint4 *v = reinterpret_cast<const uint4 *>(P.rin + nslot);
+#if PT_PARK_EARLY >= 2
+            const uint32_t slot = GEN ? 0u : WS[lane];
+#else
+            const uint32_t slot = nslot;
+#endif
+            const uint4 *v = reinterpret_cast<const uint4 *>(P.rin + slot);
             const uint4 a = v[0], b = v[1], c = v[2];
             s0 = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
             s1 = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w));
             s2 = make_float4(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w));
             s3 = v[3];
-            if (wide_of<Map>(P)) sh = P.mask_hi[nslot];
+            if (wide_of<Map>(P)) sh = P.mask_hi[slot];
         }
         if (wcnt != 0u) {
             next_window(nb, nc);
             if (!GEN && uint32_t(lane) < nc) nslot = P.idx[nb + uint32_t(lane)];
         }
     };
+#if PT_PARK_EARLY >= 2
+    if constexpr (!GEN) WS[lane] = nslot;  // (the first window's slots; no store issued yet)
+    __builtin_amdgcn_wave_barrier();
+#endif
     stage();
 
     int state = ST_FREE;
@@ -950,6 +966,9 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         if constexpr (MapWide<Map>::v != 0)
             if (wide_of<Map>(P)) W[4][lane] = make_uint4(sh.x, sh.y, 0u, 0u);
         in_lds = true;
+#if PT_PARK_EARLY >= 2
+        if constexpr (!GEN) WS[lane] = nslot;
+#endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
