@@ -312,15 +312,6 @@ __device__ __forceinline__ void bin_scan_fused(const PtPass &P, uint32_t *lds) {
 #ifndef PT_SHADE_EARLY
 #define PT_SHADE_EARLY 0
 #endif
-#ifndef PT_SHADE_GROUP
-#define PT_SHADE_GROUP 0
-#endif
-#ifndef PT_SHADE_PIPE
-#define PT_SHADE_PIPE 0
-#endif
-#ifndef PT_PARK_EARLY
-#define PT_PARK_EARLY 0
-#endif
 template <class Map, bool ST, bool TAPS>
 __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
@@ -343,11 +334,8 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     stt.init();
     const PtLaunch &L = P.L;
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
-    // `before_stores`: called once the colour slot is updated and the next
-    // segment's bounds() mask is known, before the position's key / next-ray
-    // stores (PT_SHADE_PIPE issues the next record's loads there)
     auto shade_one = [&](uint32_t i, const uint4 &q0, const uint4 &q1, const uint4 &q2, const uint4 &q3,
-                         const uint2 &hi, auto &&before_stores) {
+                         const uint2 &hi) {
         pt_f3 ro{__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
         pt_f3 rd{__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
         pt_f3 thr{__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
@@ -426,7 +414,6 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             P.color[sid] = c;
         }
         if (done) {
-            before_stores();
             if (L.debug == 3) {  // bounce-count view: the colour is the segment count, not the radiance
                 const pt_f3 col = final_color(L.debug, seg, L.bounces, ret);
                 P.color[sid] = make_float4(col.x, col.y, col.z, 0.0f);
@@ -444,7 +431,6 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             m.y |= m2.y;
         }
 #endif
-        before_stores();
         store_ray(P.rin + i, ro, rd, thr, rng, sid, 0u, make_uint4(m.x, m.y, 0u, 0u));
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);
@@ -475,7 +461,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                     const float4 nd = P.hitn[j];
                     hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
                 }
-                shade_one(j, q0, q1, q2, q3, hi, [] {});
+                shade_one(j, q0, q1, q2, q3, hi);
             }
             qh += cnt;
             qn -= cnt;
@@ -527,98 +513,6 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         if (qn > 0u) run(qn);
     } else
 #endif
-#if PT_SHADE_PIPE
-    // (A/B) The next position's record loads issued after this position's
-    // colour update and before its key / next-ray stores.  gfx950 has one
-    // vmcnt for loads and stores, retired in order, so a record load issued
-    // behind the previous position's stores (the default loop) waits for
-    // those stores to complete as well; issued ahead of them it does not.
-    // The record is loaded once the shading is done, so it does not stay live
-    // through the taps (PT_SHADE_PREFETCH held it there and spilled).
-    if constexpr (!ST) {
-        const uint32_t stride = gridDim.x * blockDim.x;
-        uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-        uint4 q0 = make_uint4(0u, 0u, 0u, 0u), q1 = q0, q2 = q0, q3 = q0;
-        uint2 hi = make_uint2(0u, 0u);
-        auto load = [&](uint32_t j, uint4 &a, uint4 &b, uint4 &c, uint4 &d, uint2 &h) {
-            a = P.rin[j].q[0], b = P.rin[j].q[1], c = P.rin[j].q[2], d = P.rin[j].q[3];
-            if (!TAPS && wide_of<Map>(P)) {
-                const float4 nd = P.hitn[j];
-                h = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
-            }
-        };
-        if (i < n) load(i, q0, q1, q2, q3, hi);
-        while (i < n) {
-            const uint32_t in = i + stride;
-            uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0, n2 = n0, n3 = n0;
-            uint2 nh = make_uint2(0u, 0u);
-            auto pre = [&] {
-                if (in < n) load(in, n0, n1, n2, n3, nh);
-            };
-            if (q2.w == PT_AUX_MISS) {
-                pre();
-                P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
-            } else {
-                shade_one(i, q0, q1, q2, q3, hi, pre);
-            }
-            q0 = n0, q1 = n1, q2 = n2, q3 = n3, hi = nh;
-            i = in;
-        }
-    } else
-#endif
-#if PT_SHADE_GROUP
-    // Hits grouped by what they hit (timed kernel, A/B): a wave's normal taps
-    // evaluate every shape any of its lanes keeps live, and the hits of a
-    // wave lie on different shapes (2.3 evaluations per tap where a lane
-    // needs 1.1).  Each block takes its 256 positions in material order (the
-    // material is the shape's index, record q2.w): an LDS counting sort of the
-    // chunk's keys, which were loaded one chunk ahead so the sort waits on no
-    // load; misses sort last.  Outputs still go to each record's own position.
-    if constexpr (!ST && NM > 0 && NM < 63) {
-        __shared__ uint32_t gcnt[64];
-        __shared__ unsigned short gperm[PT_BIN_BLOCK];
-        const uint32_t t = threadIdx.x;
-        const uint32_t stride = gridDim.x * blockDim.x;
-        auto key_of = [&](uint32_t i) -> uint32_t {
-            if (i >= n) return 63u;
-            const uint32_t m = P.rin[i].q[2].w;  // material, or PT_AUX_MISS
-            return m < uint32_t(NM) ? m : uint32_t(NM);
-        };
-        uint32_t base = blockIdx.x * blockDim.x;
-        uint32_t mk = key_of(base + t);
-        for (; base < n; base += stride) {  // (block-uniform)
-            if (t < 64u) gcnt[t] = 0u;
-            __syncthreads();
-            const uint32_t rank = atomicAdd(&gcnt[mk], 1u);
-            __syncthreads();
-            if (t < 64u) {  // exclusive prefix of the 64 counts (wave 0)
-                const uint32_t c = gcnt[t];
-                uint32_t inc = c;
-#pragma unroll
-                for (int off = 1; off < 64; off <<= 1) {
-                    const uint32_t x = uint32_t(__shfl_up(int(inc), off, 64));
-                    if (t >= uint32_t(off)) inc += x;
-                }
-                gcnt[t] = inc - c;
-            }
-            __syncthreads();
-            gperm[gcnt[mk] + rank] = (unsigned short)t;
-            __syncthreads();
-            const uint32_t i = base + gperm[t];
-            mk = key_of(base + stride + t);  // the next chunk's key, one chunk ahead
-            if (i < n) {
-                const uint4 q0 = P.rin[i].q[0], q1 = P.rin[i].q[1], q2 = P.rin[i].q[2], q3 = P.rin[i].q[3];
-                uint2 hi = make_uint2(0u, 0u);
-                if (!TAPS && wide_of<Map>(P)) {
-                    const float4 nd = P.hitn[i];
-                    hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
-                }
-                if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;
-                else shade_one(i, q0, q1, q2, q3, hi, [] {});
-            }
-        }
-    } else
-#endif
     {
     // Nearly every position holds a hit (misses end in the trace pass), so
     // each thread takes one position and loads its whole record (a miss
@@ -644,7 +538,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
         }
         if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
-        else shade_one(i, q0, q1, q2, q3, hi, [] {});
+        else shade_one(i, q0, q1, q2, q3, hi);
     }
     }
     hist_flush(lh, P.hist);
@@ -788,13 +682,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     // the staged window, once its loads have landed: [part][lane], so a
     // refill reads a ray with 4 ds_read_b128 instead of 16 cross-lane moves
     __shared__ uint4 W[MapWide<Map>::v == 0 ? 4 : 5][64];  // (W[4]: check[] bits 64..127)
-#if PT_PARK_EARLY >= 2
-    // the next window's slots, copied here when the current window is parked:
-    // staging then reads them from LDS (lgkmcnt) instead of waiting on their
-    // vector load with vmcnt(0), which also waits for every hit-record store
-    // issued since (one in-order counter for loads and stores)
-    __shared__ uint32_t WS[64];
-#endif
     const PtLaunch &L = P.L;
     const int lane = int(threadIdx.x);
     Stats<ST> st;
@@ -881,11 +768,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             s3 = make_uint4(m.x, m.y, 0u, 0u);
             sh = make_uint2(m.z, m.w);
         } else if (uint32_t(lane) < wcnt) {
-#if PT_PARK_EARLY >= 2
-            const uint32_t slot = GEN ? 0u : WS[lane];
-#else
             const uint32_t slot = nslot;
-#endif
             const uint4 *v = reinterpret_cast<const uint4 *>(P.rin + slot);
             const uint4 a = v[0], b = v[1], c = v[2];
             s0 = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
@@ -899,10 +782,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             if (!GEN && uint32_t(lane) < nc) nslot = P.idx[nb + uint32_t(lane)];
         }
     };
-#if PT_PARK_EARLY >= 2
-    if constexpr (!GEN) WS[lane] = nslot;  // (the first window's slots; no store issued yet)
-    __builtin_amdgcn_wave_barrier();
-#endif
     stage();
 
     int state = ST_FREE;
@@ -966,9 +845,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         if constexpr (MapWide<Map>::v != 0)
             if (wide_of<Map>(P)) W[4][lane] = make_uint4(sh.x, sh.y, 0u, 0u);
         in_lds = true;
-#if PT_PARK_EARLY >= 2
-        if constexpr (!GEN) WS[lane] = nslot;
-#endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1089,12 +965,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             }
         }
         tm = st.lap(PT_ST_CYC_MAP, tm);
-#if PT_PARK_EARLY
-        // (A/B) park a freshly staged window right after the map step, before
-        // this iteration's hit-record stores: waiting for its loads then does
-        // not also wait for stores issued behind them (one in-order vmcnt)
-        if (!in_lds && wcnt != 0u) park();
-#endif
 
         // ---- 3. hand finished segments on: a miss ends the path (its
         // colour slot already holds its radiance), a hit goes to the shade
