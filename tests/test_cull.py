@@ -360,3 +360,42 @@ def test_shipped_scene_kernels_survive_a_torch_first_process():
     assert _probe("c3", "1", first="torch") == _probe("c3", "1", first="none")
     assert _probe("c3", "1", first="torch")[0] is False
     assert _probe("c3", "1", first="torch", PT_JIT_CACHE="0")[0] is True
+
+
+def test_wave_fallback_is_per_kernel():
+    """pt_jit.cpp rebuilds at 7 waves only the kernels whose 8-wave build
+    spilled (PT_TW_N: march-only trace, PT_TG_N: first pass, PT_TT_N: taps
+    in the trace pass, PT_SW_N: shade beyond 16 bytes per lane); the log's
+    first line names both lists, and they must agree.  C3's table build
+    (values read from the node table) is the case that spills in part."""
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    prog = (f"import os, sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; os.environ['PT_JIT_CACHE'] = '0'; "
+            f"import test_cull as T; T.os.environ['PT_JIT_BAKE'] = '0'; "
+            f"import ctypes; from compute_path_tracer_amd import scenes, _native as N; "
+            f"from compute_path_tracer_amd.sdf_editor import CompData; p = scenes.SCENES['c3']().compile(CompData()); "
+            f"log = ctypes.create_string_buffer(1 << 16); "
+            f"rc = N.lib().pt_jit_compile(p.ops, p.n_ops, p.aabbs, p.n_aabb, "
+            f"p.data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(p.data), log, len(log), None); "
+            f"print(rc); print(log.value.decode(errors='replace').splitlines()[0])")
+    out = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rc, first = out.stdout.splitlines()[-2:]
+    assert rc == "0"
+    if not first.startswith("(rebuilt at 7 waves per SIMD"):
+        return  # (this compiler fits the whole table build in 64 VGPRs)
+    m = re.match(r"\(rebuilt at 7 waves per SIMD:((?: PT_[A-Z]{2}_N=7)+); the 8-wave build spilled, bytes/lane:(.*)\)",
+                 first)
+    assert m, first
+    lowered = set(m.group(1).split())
+    spilled = dict(kv.split("=") for kv in m.group(2).split())
+    want = set()
+    for kernel, macro in (("pt_bin_trace_m_jit", "PT_TW_N"), ("pt_bin_trace_g_jit", "PT_TG_N"),
+                          ("pt_bin_trace_jit", "PT_TT_N")):
+        if int(spilled.get(kernel, 0)) > 0:
+            want.add(macro + "=7")
+    if int(spilled.get("pt_bin_shade_t_jit", 0)) > 16:
+        want.add("PT_SW_N=7")
+    assert lowered == want, (lowered, spilled)
