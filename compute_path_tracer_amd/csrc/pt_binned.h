@@ -93,27 +93,10 @@ struct PtPass {
                             // colour slot, and the shade pass stores (not adds) the first segment's emission
     uint32_t *scan_ctrl;    // shade: non-null = the next pass's control words; the block that finishes last
                             // scans the histogram into offs and sets them (no separate scan launch)
-    int32_t skey;           // (A/B, PT_SPATIAL_KEY) 0: key = bin; 1: + the next ray's direction octant;
-                            // 2: + octant and origin cell, in bits 16..24 -- the scatter orders each tile's
-                            // rays by it before handing out bin places (spatially coherent windows per bin)
 };
 #define PT_CTRL_TICKET 16u  // control word counting a shade pass's finished blocks (fused scan)
 
 namespace pt {
-
-// spatial secondary key of a ray (PtPass.skey): direction octant (3 bits) and,
-// at 2, the origin's unit cell mod 4 per axis (6 bits), above the bin
-#define PT_SKEY_SHIFT 16
-#define PT_SKEY_N 512
-__device__ __forceinline__ uint32_t spatial_key(int mode, const pt_f3 &ro, const pt_f3 &rd) {
-    uint32_t k = (rd.x < 0.0f ? 1u : 0u) | (rd.y < 0.0f ? 2u : 0u) | (rd.z < 0.0f ? 4u : 0u);
-    if (mode >= 2) {
-        const uint32_t cx = uint32_t(int(floorf(ro.x))) & 3u, cy = uint32_t(int(floorf(ro.y))) & 3u,
-                       cz = uint32_t(int(floorf(ro.z))) & 3u;
-        k |= (cx << 3) | (cy << 5) | (cz << 7);
-    }
-    return k;
-}
 
 __device__ __forceinline__ uint32_t bin_of(const uint4 &m) {
     if ((m.y | m.z | m.w) == 0u && m.x < uint32_t(PT_BINS)) return m.x;  // small scenes: the exact set
@@ -451,7 +434,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         store_ray(P.rin + i, ro, rd, thr, rng, sid, 0u, make_uint4(m.x, m.y, 0u, 0u));
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);
-        P.key[i] = P.skey ? k | (spatial_key(P.skey, ro, rd) << PT_SKEY_SHIFT) : k;
+        P.key[i] = k;
         atomicAdd(&lh[k], 1u);
     };
 #if PT_SHADE_EARLY
@@ -626,7 +609,6 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
     // atomics that use them)
     constexpr uint32_t U = 8u;
     hist_zero(cnt);
-    const uint32_t bmask = P.skey ? (1u << PT_SKEY_SHIFT) - 1u : 0xffffffffu;  // (the bin below the spatial key)
     for (uint32_t e0 = b0 + threadIdx.x; e0 < b1; e0 += U * PT_BIN_BLOCK) {
         uint32_t k[U];
 #pragma unroll
@@ -636,7 +618,7 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
         }
 #pragma unroll
         for (uint32_t j = 0; j < U; ++j)
-            if (k[j] != PT_BIN_NONE) atomicAdd(&cnt[k[j] & bmask], 1u);
+            if (k[j] != PT_BIN_NONE) atomicAdd(&cnt[k[j]], 1u);
     }
     __syncthreads();
     for (int b = int(threadIdx.x); b < PT_BINS; b += PT_BIN_BLOCK) {
@@ -644,68 +626,6 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
         if (c != 0u) cnt[b] = atomicAdd(&P.offs[b], c);
     }
     __syncthreads();
-    if (P.skey) {
-        // each tile of U * PT_BIN_BLOCK slots in spatial-key order (an LDS
-        // counting sort), so a bin's places go to its rays key by key
-        __shared__ uint32_t sc[PT_SKEY_N];
-        __shared__ unsigned short sperm[U * PT_BIN_BLOCK];
-        const uint32_t t = threadIdx.x;
-        for (uint32_t base = b0; base < b1; base += U * PT_BIN_BLOCK) {  // (block-uniform)
-            uint32_t k[U], r[U];
-            for (uint32_t q = t; q < PT_SKEY_N; q += PT_BIN_BLOCK) sc[q] = 0u;
-            __syncthreads();
-#pragma unroll
-            for (uint32_t j = 0; j < U; ++j) {
-                const uint32_t e = base + j * PT_BIN_BLOCK + t;
-                k[j] = e < b1 ? P.key[e] : PT_BIN_NONE;
-                r[j] = k[j] != PT_BIN_NONE ? atomicAdd(&sc[k[j] >> PT_SKEY_SHIFT], 1u) : 0u;
-            }
-            __syncthreads();
-            if (t < 64u) {  // exclusive prefix of the PT_SKEY_N counts (wave 0, PT_SKEY_N / 64 each)
-                constexpr uint32_t PER = PT_SKEY_N / 64;
-                uint32_t v[PER], sum = 0u;
-#pragma unroll
-                for (uint32_t q = 0; q < PER; ++q) sum += (v[q] = sc[t * PER + q]);
-                uint32_t inc = sum;
-#pragma unroll
-                for (int off = 1; off < 64; off <<= 1) {
-                    const uint32_t x = uint32_t(__shfl_up(int(inc), off, 64));
-                    if (t >= uint32_t(off)) inc += x;
-                }
-                uint32_t run = inc - sum;
-#pragma unroll
-                for (uint32_t q = 0; q < PER; ++q) {
-                    sc[t * PER + q] = run;
-                    run += v[q];
-                }
-            }
-            __syncthreads();
-            __shared__ uint32_t tot;  // the tile's live slots
-            if (t == 0u) tot = 0u;
-            uint32_t mine = 0u;
-#pragma unroll
-            for (uint32_t j = 0; j < U; ++j)
-                if (k[j] != PT_BIN_NONE) {
-                    sperm[sc[k[j] >> PT_SKEY_SHIFT] + r[j]] = (unsigned short)(j * PT_BIN_BLOCK + t);
-                    ++mine;
-                }
-            __syncthreads();
-            if (mine) atomicAdd(&tot, mine);
-            __syncthreads();
-            const uint32_t total = tot;  // sperm[0 .. total) = the live slots in key order
-#pragma unroll
-            for (uint32_t j = 0; j < U; ++j) {
-                const uint32_t s = j * PT_BIN_BLOCK + t;
-                if (s < total) {
-                    const uint32_t li = sperm[s], e = base + li;
-                    const uint32_t kk = P.key[e] & bmask;
-                    P.idx[atomicAdd(&cnt[kk], 1u)] = e;
-                }
-            }
-            __syncthreads();
-        }
-        return;
-    }
     for (uint32_t e0 = b0 + threadIdx.x; e0 < b1; e0 += U * PT_BIN_BLOCK) {
         uint32_t k[U];
 #pragma unroll

@@ -884,12 +884,6 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             p.wide = c->n_check > 64 ? 1 : 0;
             p.run_max = run_max;
             p.refill_min = refill_min;
-            static const int skey = [] {  // A/B knob: spatial order inside each bin (PtPass.skey)
-                const char *v = std::getenv("PT_SPATIAL_KEY");
-                const int k = v ? std::atoi(v) : 0;
-                return k >= 0 && k <= 2 ? k : 0;
-            }();
-            p.skey = skey;
         }
         if (nl > 1) {  // lanes 1.. start after everything enqueued on the context stream so far
             HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
