@@ -48,6 +48,11 @@ W_AABB = 40
 W_SHADE = 100
 W_CAMERA = 25
 W_ACCUM = 10
+# Executed (not algorithmic) work of a shape evaluation the distance bound
+# dropped: the test that dropped it -- the translate
+# and scale of the transform's first steps (6), |t|^2 (5), the target's
+# margin (3) and the compare (2) -- instead of its transform, SDF and combine.
+W_CULL_TEST = 16
 
 
 def shade_flops(st: dict, taps: dict, n_aabb: int) -> float:
@@ -69,6 +74,27 @@ def trace_flops(st: dict, taps: dict, n_aabb: int, gen_trace: bool) -> float:
     rays and primary bounds()."""
     gen = 0.0 if gen_trace else (W_CAMERA + W_AABB * n_aabb) * st["samples"]
     return algorithmic_flops(st) - shade_flops(st, taps, n_aabb) - W_ACCUM * st["samples"] - gen
+
+
+def culled_flops(st: dict) -> float:
+    """Algorithmic flops of st's culled shape evaluations that did not run:
+    transform + finalise + SDF (the share's mean SDF weight: the counters do
+    not split culls by kind) + combine (1), less the W_CULL_TEST flops of the
+    test that dropped each one."""
+    n, c = st.get("xform_shape", 0), st.get("culled", 0)
+    if not n or not c:
+        return 0.0
+    sdf_mean = sum(w * st[k] for k, w in W_SDF.items()) / n
+    return float(c) * (W_XFORM + W_FINALISE + sdf_mean + 1 - W_CULL_TEST)
+
+
+def executed_split(st: dict, taps: dict, n_aabb: int, gen_trace: bool) -> tuple:
+    """(trace, shade) flops that the kernels executed: each pass's
+    algorithmic flops less its culled evaluations (culled_flops) -- the
+    trace passes' culls are st's minus the taps' (PathTracer.tap_stats)."""
+    trace_share = {k: v - taps.get(k, 0) for k, v in st.items()}
+    return (trace_flops(st, taps, n_aabb, gen_trace) - culled_flops(trace_share),
+            shade_flops(st, taps, n_aabb) - culled_flops(taps))
 
 
 def map_flops(st: dict) -> float:
@@ -187,9 +213,19 @@ def hw_view(derived: dict) -> dict:
     return out
 
 
+def cpu_quota():
+    """CPUs' worth of time the cgroup lets this process use (cpu.max), or
+    None when unlimited / not readable."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_info() -> dict:
-    """Host CPU of this box: model, logical CPUs, and the CPUs this process
-    may run on (a GPU box's share can be far below os.cpu_count())."""
+    """Host CPU of this box: model, logical CPUs, the CPUs this process may
+    run on (affinity) and the cgroup's CPU quota."""
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -202,10 +238,14 @@ def cpu_info() -> dict:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = os.cpu_count() or 1
-    return {"model": model, "os_cpu_count": os.cpu_count(), "affinity": affinity}
+    return {"model": model, "os_cpu_count": os.cpu_count(), "affinity": affinity, "quota": cpu_quota()}
 
 
-def cpu_baseline(scene, w, h, bounces, threads: int, row_stride: int, spp: int) -> dict:
+def cpu_baseline(scene, w, h, bounces, threads: int, row_stride: int, spp, target_s: float = 12.0) -> dict:
+    """The C oracle (test infrastructure: the CPU restatement of the
+    reference's per-pixel loop, pthreads) on `threads` host threads, over
+    every row_stride-th row of the same frame.  spp None: chosen from a
+    1-spp calibration run so the timed run takes about target_s seconds."""
     import tempfile
 
     from oracle import oracle as O  # test infrastructure: the CPU restatement
@@ -219,27 +259,56 @@ def cpu_baseline(scene, w, h, bounces, threads: int, row_stride: int, spp: int) 
     osc = O.OracleScene(scene.rows())
     c = O.Constants(0.0, 1, float(np.float32(w) / np.float32(h)), 1)
     s = O.Settings(0, bounces, 1.0, 1.0, 0)
-    osc.render(w, h, c, s, 1, row_stride=row_stride * 8, threads=threads)  # warm caches
+    rows = len(range(0, h, row_stride))
+    t0 = time.perf_counter()
+    osc.render(w, h, c, s, 1, row_stride=row_stride, threads=threads)  # warm caches + calibration
+    cal = time.perf_counter() - t0
+    if spp is None:
+        spp = int(max(1, min(64, round(target_s / max(cal, 1e-3)))))
     t0 = time.perf_counter()
     osc.render(w, h, c, s, spp, row_stride=row_stride, threads=threads)
     dt = time.perf_counter() - t0
-    rows = len(range(0, h, row_stride))
     samples = rows * w * spp
+    quota = info["quota"]
     return {"value": samples / dt / 1e6, "unit": "Msamples/sec", "cores": threads, "kind": "port",
             "cpu_model": info["model"], "os_cpu_count": info["os_cpu_count"], "cpus_available": info["affinity"],
-            "sample": f"C oracle ({build}, {threads} threads = the CPUs this process may use) on every "
+            "cgroup_cpu_quota": quota,
+            "sample": f"C oracle ({build}, pthreads: {threads} threads = every CPU in this process's affinity "
+                      f"mask{'' if quota is None else f'; the cgroup allows {quota} CPUs of time'}) on every "
                       f"{row_stride}th row of the same {w}x{h} {bounces}-bounce frame, {spp} spp ({samples} "
-                      f"samples, {dt:.1f} s)"}
+                      f"samples, {dt:.1f} s; spp set by a {cal:.1f} s 1-spp calibration run)"}
 
 
 def default_cpu_threads() -> int:
-    """Every CPU this process may use: the affinity mask, capped by
-    OMP_NUM_THREADS where the box sets it to its CPU share."""
-    n = cpu_info()["affinity"]
-    omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and int(omp) > 0:
-        n = min(n, int(omp))
-    return max(1, n)
+    """Every CPU this process may use (its affinity mask): the oracle runs
+    pthreads, so OMP_NUM_THREADS does not apply."""
+    return max(1, cpu_info()["affinity"])
+
+
+def solo_pipeline(pt, aspect: float, frames_step: int) -> dict:
+    """Per-kernel times for the roofline (outside the timed region): one
+    dispatch of ONE pipeline's share of a step (ceil(frames / pipelines)
+    frames, so the chunk buffers fit as they are) with bin_lanes 1.  Its trace
+    and shade passes then run alone, so each launch's HIP-event time is the
+    kernel's own -- in the timed steps the two pipelines' kernels share the
+    GPU and their event times overlap.  The instrumented twin of the same
+    frames gives their exact counters."""
+    from compute_path_tracer_amd import _native as N
+
+    lanes = int(pt.get_option("bin_lanes"))
+    frames = -(-frames_step // lanes)
+    c = N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1)
+    pt.set_option("bin_lanes", 1)
+    try:
+        st = pt.stats(c, frames)
+        taps = pt.tap_stats()
+        pt.dispatch(c, frames)
+        pt.sync()
+        return {"frames": frames, "st": st, "taps": taps, "dispatch_ms": pt.last_dispatch_ms(),
+                "trace_ms": pt.get_option("trace_ms"), "trace_n": int(pt.get_option("trace_launches")),
+                "shade_ms": pt.get_option("shade_ms"), "shade_n": int(pt.get_option("shade_launches"))}
+    finally:
+        pt.set_option("bin_lanes", lanes)
 
 
 def max_over_ranks(dist, v: float, device: str) -> float:
@@ -284,6 +353,7 @@ def strong_leg(local_rank, rank, world, mode, barrier, dist, device, steps: int,
                     settings=N.Settings(debug=0, bounces=bounces, scale=1.0, fov=1.0, aabb=0))
     pt.set_option("jit_wait", 1)
     tr = TileSplitRender(pt, rank, world, float(np.float32(w) / np.float32(h)), reduce=mode, scaling="strong")
+    rccl_ranks = pt.comm_size() if world > 1 and mode == "rccl" else None
     for _ in range(warmup):
         tr.step(spp)
         tr.reduce(0)
@@ -302,18 +372,56 @@ def strong_leg(local_rank, rank, world, mode, barrier, dist, device, steps: int,
     return {"metric": "Msamples/sec, BASELINE config 4 split over the GPUs",
             "value": round(w * h * spp * steps / dt / 1e6, 3), "unit": "Msamples/sec", "scaling": "strong",
             "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(dt * 1e3 / steps, 3),
-            "render_ms_max_rank": round(render_ms, 3), "reduce_ms": round(red, 3),
+            "render_ms_max_rank": round(render_ms, 3), "reduce_ms": round(red, 3), "rccl_ranks": rccl_ranks,
             "config": {"workload": f"c3 {w}x{h}, {bounces} bounces, {spp} spp per step over all GPUs",
                        "width": w, "height": h, "bounces": bounces, "spp_per_step": spp,
                        "parallelism": f"tiles{world}", "reduce": "RCCL ncclReduce(sum) onto rank 0"
                        if mode == "rccl" else "host sum over torch.distributed (gloo)"}}
 
 
+def free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(argv: list, n: int, port: int) -> list:
+    """The torch.distributed.run command that runs this script as n ranks
+    (one process per GPU) with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def resolve_world(gpus, env=os.environ):
+    """(world, launch): the rank count this run is for, and whether this
+    process must first start that many ranks itself.
+    - a launcher set WORLD_SIZE: it must equal --gpus when given (SystemExit
+      otherwise: the line would claim the wrong n_gpus);
+    - no launcher and --gpus N > 1: launch N ranks (bench.py starts them);
+    - otherwise one rank."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        world = int(ws)
+        if gpus is not None and gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return world, False
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {n}")
+    return n, n > 1
+
+
 def main() -> None:
     from compute_path_tracer_amd import scenes as _scenes
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks, one process each).  Without a launcher, N > 1 starts N ranks through "
+                         "torch.distributed.run; under one it must equal WORLD_SIZE.  Default: WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(_scenes.CONFIGS),
@@ -326,10 +434,13 @@ def main() -> None:
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--bounces", type=int, default=None)
     ap.add_argument("--scene", default=None)
+    ap.add_argument("--pipelines", type=int, default=None,
+                    help="binned pipelines per chunk (pt_set_option bin_lanes; default the library's 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may use")
     ap.add_argument("--cpu-row-stride", type=int, default=1)
-    ap.add_argument("--cpu-spp", type=int, default=6)
+    ap.add_argument("--cpu-spp", type=int, default=None,
+                    help="CPU baseline spp (default: sized to ~12 s by a 1-spp calibration run)")
     ap.add_argument("--c4-steps", type=int, default=2,
                     help="N > 1: steps of the config-4 strong-scaling leg (0 skips it)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -337,6 +448,15 @@ def main() -> None:
     ap.add_argument("--validate", action="store_true",
                     help="rank 0 re-renders every frame on one GPU and checks the assembled image bit for bit")
     args = ap.parse_args()
+    world, launch = resolve_world(args.gpus)
+    if launch:
+        # N ranks from one command line: torch.distributed.run as a child
+        # process, started before anything here touches the GPU (no exec);
+        # rank 0 prints the line on the shared stdout
+        import subprocess
+
+        rc = subprocess.run(launcher_cmd(sys.argv[1:], world, free_port()), cwd=ROOT).returncode
+        sys.exit(rc)
     cscene, cw, ch, cspp, cb = _scenes.CONFIGS[args.config]
     scene_name = args.scene or cscene
     width, height = args.width or cw, args.height or ch
@@ -344,7 +464,6 @@ def main() -> None:
     spp = args.spp or cspp
     scaling = "strong" if args.config == "c4" else "weak"
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("PT_BENCH_SHARE_GPU"):  # test aid: all ranks on GPU 0 (single-GPU boxes)
@@ -374,12 +493,16 @@ def main() -> None:
     prog = ed.compile(CompData())
     settings = N.Settings(debug=0, bounces=bounces, scale=1.0, fov=1.0, aabb=0)
     pt = PathTracer(width, height, prog, device=local_rank, settings=settings)
+    if args.pipelines is not None:
+        pt.set_option("bin_lanes", args.pipelines)
     # setup, untimed: install the values-baked scene kernel (jit_bake 2 tier-up;
     # an interactive caller keeps rendering on the table kernel meanwhile)
     pt.set_option("jit_wait", 1)
     aspect = float(np.float32(width) / np.float32(height))
     mode = "rccl" if args.dist_backend == "nccl" else "host"
     tr = TileSplitRender(pt, rank, world, aspect, reduce=mode, scaling=scaling)
+    # the ranks RCCL itself counts in the reduce's communicator (null: no RCCL reduce)
+    rccl_ranks = pt.comm_size() if world > 1 and mode == "rccl" else None
     spp_step = spp * world if scaling == "weak" else spp  # frames per rank per step
 
     def barrier():
@@ -428,6 +551,7 @@ def main() -> None:
         tr.step(spp)
         record_times()
     reduce_ms = reduce_probe(tr, pt, barrier, dist, dev)
+    solo = solo_pipeline(pt, aspect, spp_step) if world == 1 and trace_n else None
     validation = None
     if args.validate:
         img = tr.image(0)  # every frame rendered so far, assembled on rank 0
@@ -447,7 +571,9 @@ def main() -> None:
     out = None
     if rank == 0:
         out = report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, spp_step, world, scaling,
-                     value, ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation)
+                     value, ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation,
+                     solo)
+        out["rccl_ranks"] = rccl_ranks
     pt.close()
     if world > 1 and scaling == "weak" and args.c4_steps > 0 and not args.validate:
         leg = strong_leg(local_rank, rank, world, mode, barrier, dist, dev, args.c4_steps, 1)
@@ -461,7 +587,7 @@ def main() -> None:
 
 
 def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, spp_step, world, scaling, value,
-           ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation) -> dict:
+           ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation, solo=None) -> dict:
     """Rank 0's JSON line."""
     d_ms = float(np.mean(kernel_ms))  # one dispatch = one step's frames of this rank
     flops_step = algorithmic_flops(st)
@@ -473,28 +599,50 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
     shade_taps = bool(pt.get_option("shade_taps")) and jit
     n_aabb = prog.n_aabb
     shade = None
-    if trace_n:  # dominant kernel: the binned trace pass (flops of its passes / their device time)
+    eq = None  # the reference-equivalent view (algorithmic flops over the overlapped timed launches)
+    if trace_n:  # dominant kernel: the binned trace pass
         hot = ("pt_bin_trace_m_jit" if shade_taps else "pt_bin_trace_jit") if jit else "pt_bin_trace_kernel"
+        shade_kernel = "pt_bin_shade_t_jit" if shade_taps else "pt_bin_shade_kernel"
         launches = float(np.mean(trace_n))
         t_ms = float(np.mean(trace_ms))
-        k_ms = t_ms / launches
-        k_flops = trace_flops(st, taps, n_aabb, gen_trace)
-        achieved_tf = k_flops / (t_ms * 1e-3) / 1e12
         s_ms, s_n = float(np.mean(shade_ms)), float(np.mean(shade_n))
-        s_flops = shade_flops(st, taps, n_aabb)
-        s_tf = s_flops / (s_ms * 1e-3) / 1e12
-        shade = {"kernel": ("pt_bin_shade_t_jit" if shade_taps else "pt_bin_shade_kernel"),
+        alg_t = trace_flops(st, taps, n_aabb, gen_trace)
+        alg_s = shade_flops(st, taps, n_aabb)
+        eq = {"trace_frac": round(alg_t / (t_ms * 1e-3) / 1e12 / PEAK_F32_TFLOPS, 4),
+              "shade_frac": round(alg_s / (s_ms * 1e-3) / 1e12 / PEAK_F32_TFLOPS, 4),
+              "trace_ms_per_launch": round(t_ms / launches, 3), "shade_ms_per_launch": round(s_ms / max(1.0, s_n), 3),
+              "timing": f"the timed steps: {int(pt.get_option('bin_lanes'))} pipelines, whose kernels share the GPU "
+                        "(their launches' event times overlap)",
+              "flops": "algorithmic: every counted event at its SURVEY 8(d) weight, culled evaluations included "
+                       "(what the reference's loop would execute)"}
+        # executed flops over each kernel's own time: the one-pipeline run
+        # (solo_pipeline) when there is one, else the timed steps
+        if solo is not None:
+            ex_t, ex_s = executed_split(solo["st"], solo["taps"], n_aabb, gen_trace)
+            tk_ms, tk_n, sk_ms, sk_n = solo["trace_ms"], solo["trace_n"], solo["shade_ms"], solo["shade_n"]
+            timing = (f"one pipeline alone (bin_lanes 1, {solo['frames']} frames = one pipeline's share of a "
+                      "step, outside the timed region): HIP events around each launch on its stream")
+        else:
+            ex_t, ex_s = executed_split(st, taps, n_aabb, gen_trace)
+            tk_ms, tk_n, sk_ms, sk_n = t_ms, launches, s_ms, s_n
+            timing = eq["timing"]
+        achieved_tf = ex_t / (tk_ms * 1e-3) / 1e12
+        s_tf = ex_s / (sk_ms * 1e-3) / 1e12
+        k_flops, k_ms, kl = ex_t, tk_ms / max(1.0, tk_n), tk_n
+        shade = {"kernel": shade_kernel,
                  "achieved": round(s_tf, 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                 "frac": round(s_tf / PEAK_F32_TFLOPS, 4), "flops_per_step": round(s_flops),
-                 "flops_per_launch": round(s_flops / max(1.0, s_n)), "ms_per_launch": round(s_ms / max(1.0, s_n), 3),
-                 "launches_per_step": s_n, "ms_per_step_summed": round(s_ms, 3),
+                 "frac": round(s_tf / PEAK_F32_TFLOPS, 4), "executed_flops_per_launch": round(ex_s / max(1.0, sk_n)),
+                 "ms_per_launch": round(sk_ms / max(1.0, sk_n), 3), "launches": sk_n,
+                 "ms_per_step_summed": round(s_ms, 3), "launches_per_step": s_n,
                  "scope": "calc_normal's six taps (map() work + 29), bounds() of continuing rays (40 per slab test) "
-                          "and shading + RR (100 per hit) / the shade launches' HIP-event time"}
+                          "and shading + RR (100 per hit), less culled tap evaluations"}
     else:  # the tile-resident kernels do the whole path in one launch
         hot = "pt_wave_jit" if jit else "pt_wave_kernel"
-        launches, t_ms, k_ms = 1.0, d_ms, d_ms
-        k_flops = flops_step
-        achieved_tf = flops_step / (d_ms * 1e-3) / 1e12
+        launches = kl = 1.0
+        k_ms = d_ms
+        k_flops = flops_step - culled_flops(st)
+        achieved_tf = k_flops / (d_ms * 1e-3) / 1e12
+        timing = "the timed dispatches (one kernel)"
     path_tf = flops_step / (d_ms * 1e-3) / 1e12
     achieved_gbs = pipe["total"] / (d_ms * 1e-3) / 1e9  # whole dispatch: every pass's algorithmic bytes
     data = f"synthetic (scenes.{scenes_fn(scene_name)}"
@@ -524,8 +672,11 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
                      "kernel": hot, "achieved": round(achieved_tf, 3), "peak": PEAK_F32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_TFLOPS, 4), "traffic": None,
                      "traffic_source": None,
+                     "flops": "executed: the counted events at their SURVEY 8(d) weights, less each culled shape "
+                              f"evaluation's transform + SDF + combine (a culled one costs its {W_CULL_TEST}-flop test)",
+                     "timing": timing,
                      "algorithmic_flops_per_sample": round(flops_step / max(1, st["samples"]), 1),
-                     "kernel_flops_per_launch": round(k_flops / launches),
+                     "kernel_flops_per_launch": round(k_flops / max(1.0, kl)),
                      "kernel_scope": "trace passes (the first with its camera rays and primary bounds()): march "
                                      "map() work + 10 per step" if gen_trace else "trace passes: march",
                      "kernel_ms_per_launch": round(k_ms, 3), "kernel_launches_per_step": launches,
@@ -547,10 +698,17 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
                 "tier_active": bool(pt.get_option("jit_tier_active")),
                 "tier_compile_s": round(pt.get_option("jit_tier_seconds"), 3),
                 "trace_waves_per_simd": pt.get_option("jit_trace_waves"),
+                # 1: the scene kernels came from the shipped cache (lib/jitcache), 0: this process compiled them
+                "from_shipped_cache": int(pt.get_option("jit_cache")),
                 "shade_waves_per_simd": pt.get_option("jit_shade_waves")},
     }
     if shade is not None:
         out["roofline"]["shade"] = shade
+        # the two kernels' fractions of the same peak, each over its own time
+        out["roofline"]["fracs_sum"] = round(out["roofline"]["frac"] + shade["frac"], 4)
+    if eq is not None:
+        out["roofline"]["reference_equivalent"] = eq
+        out["roofline"]["reference_equivalent_frac"] = eq["trace_frac"]
     if world > 1:
         out["reduce_ms"] = round(reduce_ms, 3)
     if validation is not None:

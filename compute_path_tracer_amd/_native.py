@@ -47,7 +47,7 @@ SYMBOLS = (
     "pt_dispatch_stats", "pt_set_option", "pt_get_option", "pt_jit_log", "pt_jit_compile", "pt_last_error",
     "pt_destroy", "pt_abi_version", "pt_device_math", "pt_check_sqrt_exhaustive", "pt_check_div_exhaustive",
     "pt_check_div_random", "pt_check_box_random", "pt_check_div_k", "pt_display", "pt_write_accum",
-    "pt_compile_scene_keyed", "pt_save_rgba8",
+    "pt_compile_scene_keyed", "pt_save_rgba8", "pt_comm_size",
 )
 PT_MATH = {"max": 0, "min": 1, "sqrt": 2, "sqrtf": 3, "sin": 4, "cos": 5, "div": 6, "fma": 7}
 
@@ -138,6 +138,7 @@ def lib() -> ctypes.CDLL:
         "pt_get_size": (c_int, [ctx, u32p, u32p]),
         "pt_comm_get_unique_id": (c_int, [POINTER(c_uint8)]),
         "pt_comm_init": (c_int, [ctx, c_uint32, c_uint32, POINTER(c_uint8)]),
+        "pt_comm_size": (c_int, [ctx, u32p]),
         "pt_reduce_accum": (c_int, [ctx, c_int]),
         "pt_read_reduced": (c_int, [ctx, POINTER(c_float), c_size_t]),
         "pt_sync": (c_int, [ctx]),

@@ -91,10 +91,7 @@ struct PtPass {
     int32_t gen_trace;      // first pass without a gen pass (scene kernels, generation order): the trace
                             // pass makes each window's camera rays and bounds() itself, a miss zeroes its
                             // colour slot, and the shade pass stores (not adds) the first segment's emission
-    uint32_t *scan_ctrl;    // shade: non-null = the next pass's control words; the block that finishes last
-                            // scans the histogram into offs and sets them (no separate scan launch)
 };
-#define PT_CTRL_TICKET 16u  // control word counting a shade pass's finished blocks (fused scan)
 
 namespace pt {
 
@@ -245,52 +242,6 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
     flush_stats<ST>(L, st);
 }
 
-// The histogram scan of bin_scan_body, done by the shade pass's last block
-// to finish (a ticket on scan_ctrl[PT_CTRL_TICKET]) instead of a one-wave
-// kernel launched after it: that launch needed a free wave slot while the
-// other pipeline's shade blocks filled every CU (up to 0.4 ms per pass on a
-// C2 render).  The counts are read (and zeroed) with atomic exchanges -- the
-// other blocks' flushes are device-scope atomics.  lds: PT_BIN_BLOCK words.
-__device__ __forceinline__ void bin_scan_fused(const PtPass &P, uint32_t *lds) {
-    __shared__ uint32_t last;
-    // the block's histogram atomics performed before its ticket: a wait for
-    // the thread's outstanding vector-memory operations (no-return atomics
-    // stay counted in vmcnt until done), not a release fence, whose L2
-    // write-back in every block cost a C2 render 45 %
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(P.scan_ctrl + PT_CTRL_TICKET, 1u) == gridDim.x - 1u ? 1u : 0u;
-    __syncthreads();
-    if (!last) return;
-    constexpr int PER = PT_BINS / PT_BIN_BLOCK;
-    const int t = int(threadIdx.x);
-    uint32_t v[PER], sum = 0u;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        v[j] = atomicExch(P.hist + t * PER + j, 0u);  // (zeroed for the next pass)
-        sum += v[j];
-    }
-    uint32_t inc = sum;  // inclusive prefix within the wave
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t x = uint32_t(__shfl_up(int(inc), off, 64));
-        if ((t & 63) >= off) inc += x;
-    }
-    if ((t & 63) == 63) lds[t >> 6] = inc;  // wave totals
-    __syncthreads();
-    uint32_t base = 0u;
-    for (int w = 0; w < (t >> 6); ++w) base += lds[w];
-    uint32_t run = base + inc - sum;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        P.offs[t * PER + j] = run;
-        run += v[j];
-    }
-    if (t == PT_BIN_BLOCK - 1) P.scan_ctrl[0] = run;  // the next pass's ray count
-    if (t < PT_RUN_SHARDS) P.scan_ctrl[PT_CTRL_CURSOR(t)] = 0u;
-    if (t == 0) P.scan_ctrl[PT_CTRL_TICKET] = 0u;
-}
-
 // shade: every hit the last trace pass wrote (positions marked HIT) is
 // shaded -- material, new direction, emission, throughput, Russian roulette
 // (pt_path.h shade_lane, the same f32 steps and rng draws) -- and a path that
@@ -305,13 +256,6 @@ __device__ __forceinline__ void bin_scan_fused(const PtPass &P, uint32_t *lds) {
 // together, and the per-hit map() bound (pt_path.h tap_bound, from the hit
 // record) lets each tap drop every shape that provably lies farther away
 // (DESIGN.md 3.13).
-// PT_SHADE_EARLY=1 (A/B, default 0): the shade pass decides early ends
-// before the taps and compacts the rest (bin_shade_body).  Measured equal
-// alone (68.9 vs 68.6 ms per step) and −1.5 % with two pipelines: the second
-// load of each queued record costs what the skipped taps and slab tests save
-#ifndef PT_SHADE_EARLY
-#define PT_SHADE_EARLY 0
-#endif
 template <class Map, bool ST, bool TAPS>
 __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
@@ -377,27 +321,6 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                 }
             }
             stt.add(PT_ST_NORMAL_MAPS, 6);
-#ifdef PT_EXP_TAPS2  // timing experiment: the six taps twice (the marginal cost of the taps)
-            {
-                pt_f3 r2 = ro;
-                __asm__ volatile("" : "+v"(r2.x), "+v"(r2.y), "+v"(r2.z));
-                Check ck2{uint64_t(q3.x) | (uint64_t(q3.y) << 32), uint64_t(hi.x) | (uint64_t(hi.y) << 32)};
-                uint64_t live2 = 0ull;
-                float dp2 = 0.0f;
-                uint32_t acc = 0u;
-#pragma unroll 1
-                for (int k = 0; k < 6; ++k) {
-                    float qx, qy, qz;
-                    map_point(ST_NORMAL, k, r2, rd, 0.0f, qx, qy, qz);
-                    const Hit h = k == 0 ? Map::template first<ST>(L, qx, qy, qz, ck2, bnd, bndw, live2, stt)
-                                         : Map::template rest<ST>(L, qx, qy, qz, ck2, bnd, bndw, live2, stt);
-                    if (k == 0) ck2.alo = Map::alive(live2);
-                    if ((k & 1) == 0) dp2 = h.d;
-                    else acc |= __float_as_uint(dp2 - h.d) ^ __float_as_uint(k == 1 ? dv0 : (k == 3 ? dv1 : dv2));
-                }
-                dv0 = __uint_as_float(__float_as_uint(dv0) | acc);  // (acc = 0: the same differences)
-            }
-#endif
         }
         const bool done = shade_lane<ST>(mats, L.bounces, mat, dv0, dv1, dv2, 0, rng, ro, rd, thr, ret, seg, st);
         // ret += emission * throughput (test_compute.glsl:148) on the colour
@@ -421,117 +344,18 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             P.key[i] = PT_BIN_NONE;
             return;
         }
-        uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
-#ifdef PT_EXP_BOUNDS2  // timing experiment: bounds() twice (the marginal cost of its slab tests)
-        {
-            pt_f3 o2 = ro;
-            __asm__ volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
-            const uint4 m2 = MapBounds<Map>::template mask<ST>(L, o2, rd, st);
-            m.x |= m2.x;  // (the same bits; the compiler cannot tell)
-            m.y |= m2.y;
-        }
-#endif
+        const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
         store_ray(P.rin + i, ro, rd, thr, rng, sid, 0u, make_uint4(m.x, m.y, 0u, 0u));
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);
         P.key[i] = k;
         atomicAdd(&lh[k], 1u);
     };
-#if PT_SHADE_EARLY
-    // Early ends (timed kernel; the instrumented one keeps the reference's
-    // work: every hit taps, as the oracle counts it).  Whether a hit's path
-    // ends here -- Russian roulette, the bounce limit -- and its emission do
-    // not depend on the normal (shade_lane: the draws, the throughput update
-    // and the roulette use only the record's throughput, rng and material),
-    // so each wave first decides that for 64 positions from two of the
-    // record's four words, finishes the ending paths (colour slot, no bin)
-    // and queues the others in LDS; full waves of those then tap, shade and
-    // take bounds(): the ~30 % of hits that end (C3) no longer idle through
-    // the taps and the slab tests.
-    if constexpr (!ST) {
-        __shared__ uint32_t sq[PT_BIN_BLOCK / 64][128];  // per wave: a ring of queued positions
-        const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
-        uint32_t qh = 0u, qn = 0u;  // (wave-uniform)
-        auto run = [&](uint32_t cnt) {
-            if (ln < cnt) {
-                const uint32_t j = sq[wv][(qh + ln) & 127u];
-                const uint4 q0 = P.rin[j].q[0], q1 = P.rin[j].q[1], q2 = P.rin[j].q[2], q3 = P.rin[j].q[3];
-                uint2 hi = make_uint2(0u, 0u);
-                if (!TAPS && wide_of<Map>(P)) {
-                    const float4 nd = P.hitn[j];
-                    hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
-                }
-                shade_one(j, q0, q1, q2, q3, hi);
-            }
-            qh += cnt;
-            qn -= cnt;
-        };
-        const uint32_t stride = gridDim.x * blockDim.x;
-        for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
-            const uint32_t i = base + ln;
-            bool queue = false;
-            if (i < n) {
-                const uint4 q1 = P.rin[i].q[1], q2 = P.rin[i].q[2];
-                if (q2.w == PT_AUX_MISS) {
-                    P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
-                } else {
-                    // shade_lane's own decision, with a stand-in normal (it
-                    // changes the next direction only) and no counters
-                    pt_f3 thr{__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
-                    pt_f3 ro{0.0f, 0.0f, 0.0f}, rd{0.0f, 0.0f, 1.0f}, ret{0.0f, 0.0f, 0.0f};
-                    uint32_t rng = q2.y;
-                    int seg = P.bounce;
-                    Stats<false> none;
-                    if (shade_lane<false>(mats, L.bounces, int(q2.w), 0.0f, 0.0f, 1.0f, 0, rng, ro, rd, thr, ret, seg,
-                                          none)) {
-                        const uint32_t sid = q2.z;
-                        if (P.gen_trace) {
-                            P.color[sid] = make_float4(ret.x, ret.y, ret.z, 0.0f);
-                        } else if (ret.x != 0.0f || ret.y != 0.0f || ret.z != 0.0f) {
-                            float4 c = P.color[sid];
-                            c.x += ret.x;
-                            c.y += ret.y;
-                            c.z += ret.z;
-                            P.color[sid] = c;
-                        }
-                        if (L.debug == 3) {
-                            const pt_f3 col = final_color(L.debug, seg, L.bounces, ret);
-                            P.color[sid] = make_float4(col.x, col.y, col.z, 0.0f);
-                        }
-                        P.key[i] = PT_BIN_NONE;
-                    } else {
-                        queue = true;
-                    }
-                }
-            }
-            const uint64_t qm = __ballot(queue);
-            if (queue) sq[wv][(qh + qn + uint32_t(lane_rank(qm))) & 127u] = i;
-            qn += uint32_t(__popcll(qm));
-            __builtin_amdgcn_wave_barrier();
-            if (qn >= 64u) run(64u);
-        }
-        if (qn > 0u) run(qn);
-    } else
-#endif
-    {
     // Nearly every position holds a hit (misses end in the trace pass), so
     // each thread takes one position and loads its whole record (a miss
     // marks its record's q2): one memory round trip.
-#ifdef PT_SHADE_PREFETCH  // A/B: the next position's record loaded before this one is shaded
-    const uint32_t stride = gridDim.x * blockDim.x;
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint4 p0 = make_uint4(0u, 0u, 0u, 0u), p1 = p0, p2 = p0, p3 = p0;
-    if (i < n) p0 = P.rin[i].q[0], p1 = P.rin[i].q[1], p2 = P.rin[i].q[2], p3 = P.rin[i].q[3];
-    for (; i < n; i += stride) {
-        const uint4 q0 = p0, q1 = p1, q2 = p2, q3 = p3;
-        if (i + stride < n) {
-            const PtRay *nx = P.rin + i + stride;
-            p0 = nx->q[0], p1 = nx->q[1], p2 = nx->q[2], p3 = nx->q[3];
-        }
-#else
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint4 q0 = P.rin[i].q[0], q1 = P.rin[i].q[1], q2 = P.rin[i].q[2], q3 = P.rin[i].q[3];
-#endif
         uint2 hi = make_uint2(0u, 0u);
         if (!TAPS && wide_of<Map>(P)) {
             const float4 nd = P.hitn[i];
@@ -540,9 +364,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
         else shade_one(i, q0, q1, q2, q3, hi);
     }
-    }
     hist_flush(lh, P.hist);
-    if (P.scan_ctrl) bin_scan_fused(P, lh);
     flush_stats<ST>(L, st);
     if constexpr (!TAPS) flush_stats<ST>(L, stt, PT_ST_COUNT);
 }
@@ -592,13 +414,9 @@ __device__ __forceinline__ void bin_scan_body(const PtPass &P) {
 
 // scatter: ray slots into bin order.  Per block tile, the slots of one bin
 // take consecutive places (LDS ranks) after one global reservation.
-#ifndef PT_SCATTER_V
-#define PT_SCATTER_V 2
-#endif
 __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
     __shared__ uint32_t cnt[PT_BINS];
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
-#if PT_SCATTER_V == 2
     // One contiguous run of the slots per block: count its bins in LDS,
     // reserve each bin's places with one global atomic for the whole run
     // (not one per 4096-slot tile), then read the keys again and hand out
@@ -636,29 +454,6 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
 #pragma unroll
         for (uint32_t j = 0; j < U; ++j)
             if (k[j] != PT_BIN_NONE) P.idx[atomicAdd(&cnt[k[j]], 1u)] = e0 + j * PT_BIN_BLOCK;
-    }
-    return;
-#endif
-    const uint32_t tile = PT_BIN_BLOCK * PT_SCATTER_ITEMS;
-    for (uint32_t t0 = blockIdx.x * tile; t0 < n; t0 += gridDim.x * tile) {
-        hist_zero(cnt);
-        uint32_t kk[PT_SCATTER_ITEMS], rr[PT_SCATTER_ITEMS];
-#pragma unroll
-        for (int j = 0; j < PT_SCATTER_ITEMS; ++j) {
-            const uint32_t e = t0 + uint32_t(j * PT_BIN_BLOCK) + threadIdx.x;
-            kk[j] = e < n ? P.key[e] : PT_BIN_NONE;
-            rr[j] = kk[j] != PT_BIN_NONE ? atomicAdd(&cnt[kk[j]], 1u) : 0u;
-        }
-        __syncthreads();
-        for (int b = int(threadIdx.x); b < PT_BINS; b += PT_BIN_BLOCK) {
-            const uint32_t c = cnt[b];
-            if (c != 0u) cnt[b] = atomicAdd(&P.offs[b], c);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < PT_SCATTER_ITEMS; ++j)
-            if (kk[j] != PT_BIN_NONE) P.idx[cnt[kk[j]] + rr[j]] = t0 + uint32_t(j * PT_BIN_BLOCK) + threadIdx.x;
-        __syncthreads();
     }
 }
 
@@ -827,11 +622,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         const bool in_win = uint32_t(lane) < wcnt;
         ck.alo = wave_or_u64((mapping_now ? ck.lo : 0ull) |
                              (in_win ? (uint64_t(s3.x) | (uint64_t(s3.y) << 32)) : 0ull));
-#ifdef PT_JIT_AAND_ON
-        // and the bits all of them share: AND = ~OR(~m) (lanes outside add 0)
-        ck.aand = ~wave_or_u64((mapping_now ? ~ck.lo : 0ull) |
-                               (in_win ? ~(uint64_t(s3.x) | (uint64_t(s3.y) << 32)) : 0ull));
-#endif
         ck.ahi = wide_of<Map>(P) ? wave_or_u64((mapping_now ? ck.hi : 0ull) |
                                       (in_win ? (uint64_t(sh.x) | (uint64_t(sh.y) << 32)) : 0ull))
                         : 0ull;
@@ -852,15 +642,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
 
     for (;;) {
         uint64_t tm = st.clk();
-#ifdef PT_DEFER_STORE
-        // ---- 0. finished segments handed on together with the refill
-        {
-            const uint64_t donem = __ballot(state == ST_FREE || state == ST_SHADE);
-            if (donem != 0ull && (__popcll(donem) >= P.refill_min ||
-                                  __ballot(state == ST_MARCH || state == ST_NORMAL) == 0ull))
-                hand_on();
-        }
-#endif
         // ---- 1. refill free lanes from the staging window --------------
         const uint64_t freem = __ballot(state == ST_FREE);
         if (freem != 0ull && wcnt != 0u &&
@@ -909,11 +690,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             }
             wtake += take;
             if (wtake == wcnt) stage();  // wcnt = 0: no rays left for this wave
-#ifdef PT_REFILL_LGKM
-            // the window's LDS reads have landed before map() starts, so the
-            // shape blocks need no lgkmcnt waits of their own
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-#endif
         }
         const bool more = wcnt != 0u;
         tm = st.lap(PT_ST_CYC_REFILL, tm);
@@ -932,29 +708,6 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 map_point(TAPS ? state : int(ST_MARCH), step, ro, rd, t, qx, qy, qz);
                 uint64_t live = 0;  // (the taps' live mask: unused here)
                 const Hit h = Map::template eval<ST>(L, qx, qy, qz, ck, __builtin_inff(), __builtin_inff(), live, st);
-#if defined(PT_EXP_VALUPAD) || defined(PT_EXP_SALUPAD) || defined(PT_EXP_NOPPAD)  // timing probes: N extra independent VALU / SALU / `s_nop 1` per map
-                {
-#ifdef PT_EXP_VALUPAD
-                    float a0 = qx, a1 = qy, a2 = qz, a3 = t;
-#pragma unroll
-                    for (int k = 0; k < PT_EXP_VALUPAD / 4; ++k)
-                        __asm__ volatile("v_add_f32 %0, %0, 1.0\n v_add_f32 %1, %1, 1.0\n v_add_f32 %2, %2, 1.0\n"
-                                         " v_add_f32 %3, %3, 1.0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
-                    __asm__ volatile("" ::"v"(a0), "v"(a1), "v"(a2), "v"(a3));
-#endif
-#ifdef PT_EXP_SALUPAD
-                    uint32_t s0 = uint32_t(__builtin_amdgcn_readfirstlane(step)), s1 = s0 + 1u;
-#pragma unroll
-                    for (int k = 0; k < PT_EXP_SALUPAD / 2; ++k)
-                        __asm__ volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1));
-                    __asm__ volatile("" ::"s"(s0), "s"(s1));
-#endif
-#ifdef PT_EXP_NOPPAD
-#pragma unroll
-                    for (int k = 0; k < PT_EXP_NOPPAD; ++k) __asm__ volatile("s_nop 1");
-#endif
-                }
-#endif
                 after_map<ST, !TAPS>(h, state, step, t, ro, rd, mat, dv0, dv1, dv2, st);
                 if constexpr (!TAPS) {
                     if (state == ST_NORMAL) {  // hit: the shade pass takes the taps
@@ -968,12 +721,8 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
 
         // ---- 3. hand finished segments on: a miss ends the path (its
         // colour slot already holds its radiance), a hit goes to the shade
-        // pass as one 64 B record (PtRay).  PT_DEFER_STORE: at the next
-        // refill instead (step 0), so the stores' branch runs once for
-        // several finished lanes rather than in nearly every iteration
-#ifndef PT_DEFER_STORE
+        // pass as one 64 B record (PtRay)
         hand_on();
-#endif
         tm = st.lap(PT_ST_CYC_SHADE, tm);
         if (!more && __ballot(state != ST_FREE) == 0ull) break;
     }

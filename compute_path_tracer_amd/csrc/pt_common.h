@@ -39,9 +39,6 @@ struct Check {  // check[] of the generated bounds(), one bit per entry
     // this mask, wave-uniform (scene kernels test it first: a shape no lane
     // needs is skipped by a scalar branch); all ones = no information
     uint64_t alo = ~0ull, ahi = ~0ull;
-    // a subset of the check[] bits every such lane has (bits 0..63; 0 = no
-    // information): a shape set here needs no lane test
-    uint64_t aand = 0ull;
 };
 // a lane's check[] bit behind the wave-uniform test of Check.alo/ahi: the
 // empty volatile asm keeps the compiler from merging the two tests into one
@@ -155,13 +152,13 @@ __device__ __forceinline__ void xform(const PtNode &n, float &x, float &y, float
 // are +0) and sqrt(RN(m^2)) = m exactly (binary RN; checked for every
 // significand), so length(max(q, 0)) = m without the squares and the sqrt.
 // A wave takes that path when all its active lanes qualify.
-#if (defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)) && !defined(PT_NO_BARE_MINMAX)
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
 // max(x, 0), min(x, 0), max3 and med3 as the bare instructions.  fmaxf's
 // IEEE-mode lowering first quiets each operand produced in another basic
 // block (one `v_max_f32 v, v, v` each; the cube's q comes from before the
 // cull branch).  No operand here is a signalling NaN, and for the rest (quiet
 // NaN included: the other operand) the instructions return fmaxf's / fminf's
-// / fmed3's values.  PT_NO_BARE_MINMAX: the builtins (A/B).
+// / fmed3's values (DESIGN.md 5 history, round 3).
 __device__ __forceinline__ float pt_max0(float x) {
     float r;
     __asm__("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
@@ -200,16 +197,8 @@ __device__ __forceinline__ float cube_from_q(float qx, float qy, float qz, float
         if (__ballot(!easy) == 0ull) return m + mq;
     }
     return pt_sqrt(mx * mx + my * my + mz * mz) + mq;
-#else
+#else  // host
     const float mx = pt_gmax(qx, 0.0f), my = pt_gmax(qy, 0.0f), mz = pt_gmax(qz, 0.0f);
-#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
-    if constexpr (FAST) {
-        const float m = pt_gmax(mx, pt_gmax(my, mz));
-        const bool easy = __builtin_amdgcn_fmed3f(mx, my, mz) == 0.0f &&
-                          (m == 0.0f || __builtin_amdgcn_fmed3f(m, 0x1p-60f, 0x1p60f) == m);
-        if (__ballot(!easy) == 0ull) return m + pt_gmin(qm, 0.0f);
-    }
-#endif
     return pt_sqrt(mx * mx + my * my + mz * mz) + pt_gmin(qm, 0.0f);
 #endif
 }
@@ -233,17 +222,6 @@ __device__ __forceinline__ float sdf_k(const PtNode &n, float x, float y, float 
         const float s = n.size[0];
         const float ax = fabsf(x), ay = fabsf(y), az = fabsf(z);
         const float m = ax + ay + az - s;
-#if (defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)) && defined(PT_OCT_SELECT)
-        // the same values by selects: no exec-mask regions for the branches
-        const bool c1 = 3.0f * ax < m, c2 = 3.0f * ay < m, c3 = 3.0f * az < m;
-        const float q0 = c1 ? ax : (c2 ? ay : az);
-        const float q1 = c1 ? ay : (c2 ? az : ax);
-        const float q2 = c1 ? az : (c2 ? ax : ay);
-        const float k = pt_gmin(pt_gmax(0.5f * (q2 - q1 + s), 0.0f), s);
-        const float vy = q1 - s + k, vz = q2 - k;
-        const float len = pt_sqrt(q0 * q0 + vy * vy + vz * vz);
-        return (c1 | c2 | c3) ? len : m * 0.57735027f;
-#else
         float q0, q1, q2;
         if (3.0f * ax < m) {
             q0 = ax; q1 = ay; q2 = az;
@@ -257,7 +235,6 @@ __device__ __forceinline__ float sdf_k(const PtNode &n, float x, float y, float 
         const float k = pt_gmin(pt_gmax(0.5f * (q2 - q1 + s), 0.0f), s);
         const float vy = q1 - s + k, vz = q2 - k;
         return pt_sqrt(q0 * q0 + vy * vy + vz * vz);
-#endif
     }
 }
 __device__ __forceinline__ float sdf(const PtNode &n, float x, float y, float z) {

@@ -49,7 +49,8 @@ struct PtJitModule {
 std::string pt_jit_source(const std::vector<PtNode> &nodes, const std::vector<PtAabb> &boxes, bool fast_bounds,
                           bool bake);
 // Compile with hipRTC for gfx950; returns the code object or an error log.
-bool pt_jit_compile_source(const std::string &src, std::vector<char> &code, std::string &log);
+// on-disk cache first (*from_disk: the code object came from lib/jitcache)
+bool pt_jit_compile_source(const std::string &src, std::vector<char> &code, std::string &log, bool *from_disk = nullptr);
 // Load a code object on the current device.
 bool pt_jit_load(const std::vector<char> &code, PtJitModule &m, std::string &err);
 void pt_jit_unload(PtJitModule &m);

@@ -12,8 +12,10 @@
 // powf (glibc on Linux), which is what this file calls.  `as u8` from a
 // float saturates: NaN and values <= 0 give 0, values >= 255 give 255,
 // everything else truncates towards zero.  Host code only.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -52,11 +54,21 @@ extern "C" int pt_save_rgba8(const float *rgba, uint32_t width, uint32_t height,
         save_rows(rgba, width, height, out, 0, height, g);
         return PT_OK;
     }
+    // rows [y0 of band t, ...) per thread; a band whose thread cannot be
+    // started runs on the calling thread (no exception crosses the C ABI)
     std::vector<std::thread> pool;
-    for (uint32_t t = 0; t < threads; ++t) {
-        const uint32_t y0 = uint32_t(uint64_t(height) * t / threads), y1 = uint32_t(uint64_t(height) * (t + 1) / threads);
-        pool.emplace_back(save_rows, rgba, width, height, out, y0, y1, g);
+    uint32_t t = 0;
+    try {
+        pool.reserve(threads);
+        for (; t < threads; ++t) {
+            const uint32_t y0 = uint32_t(uint64_t(height) * t / threads);
+            const uint32_t y1 = uint32_t(uint64_t(height) * (t + 1) / threads);
+            pool.emplace_back(save_rows, rgba, width, height, out, y0, y1, g);
+        }
+    } catch (const std::exception &) {
+        // (std::system_error from std::thread, std::bad_alloc from reserve)
     }
+    save_rows(rgba, width, height, out, uint32_t(uint64_t(height) * t / threads), height, g);
     for (auto &th : pool) th.join();
     return PT_OK;
 }

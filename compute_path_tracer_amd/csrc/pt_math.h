@@ -101,10 +101,6 @@ PT_HD float pt_sqrt(float x) {
     // (zeros, negatives, tiny, inf, NaN) takes the IEEE sqrtf for the wave.
     // The fast result is formed first and replaced afterwards (one rarely
     // taken branch, no flow block around the common path).
-#ifdef PT_EXP_SQRT_OLD  // A/B (PT_JIT_DEFS): range test first, as before
-    if (__builtin_expect(__ballot((__float_as_uint(x) - 0x0F800000u) >= (0x7F800000u - 0x0F800000u)) != 0ull, 0))
-        return sqrtf(x);
-#endif
     const float y = __builtin_amdgcn_rsqf(x);
     const float g = x * y;
     const float h = 0.5f * y;

@@ -99,22 +99,8 @@ __device__ __forceinline__ bool ray_box_ulp(const PtAabb &bx, float ox, float oy
     const float tminz = (bx.bmin[2] - oz) * yz, tmaxz = (bx.bmax[2] - oz) * yz;
     const float tnear = pt_gmax(pt_gmax(pt_gmin(tminx, tmaxx), pt_gmin(tminy, tmaxy)), pt_gmin(tminz, tmaxz));
     const float tfar = pt_gmin(pt_gmin(pt_gmax(tminx, tmaxx), pt_gmax(tminy, tmaxy)), pt_gmax(tminz, tmaxz));
-#ifdef PT_ULP_MED3
-    // tnear < tfar && tfar > 0 as one compare, max(tnear, 0) < tfar, with the
-    // 0 folded into each axis as med3(tmin, tmax, 0): it equals max(min(tmin,
-    // tmax), 0) unless both values are negative, and then max(tmin, tmax) < 0
-    // bounds tfar from above and below tnear0 alike (a miss either way).  The
-    // med3 is monotone in each value, so the ulp argument carries over.
-    const float tnear0 = pt_gmax(pt_gmax(__builtin_amdgcn_fmed3f(tminx, tmaxx, 0.0f),
-                                         __builtin_amdgcn_fmed3f(tminy, tmaxy, 0.0f)),
-                                 __builtin_amdgcn_fmed3f(tminz, tmaxz, 0.0f));
-    (void)tnear;
-    gapu = min(gapu, pt_absdiff_u32<SAD>(__float_as_uint(tfar), __float_as_uint(tnear0)));
-    return tnear0 < tfar;
-#else
     gapu = min(gapu, pt_absdiff_u32<SAD>(__float_as_uint(tfar), __float_as_uint(tnear)));
     return tnear < tfar && tfar > 0.0f;
-#endif
 }
 
 // The slab test from one fma per slab: t' = RN(b * y + n) with n = -RN(o * y)

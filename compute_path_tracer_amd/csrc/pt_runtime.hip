@@ -34,6 +34,15 @@ static_assert(sizeof(pt_aabb) == 14 * 4, "pt_aabb layout");
 static_assert(sizeof(pt_scene_node) == 33 * 4, "pt_scene_node layout");
 static_assert(PT_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "RCCL unique id size");
 
+// A scene-kernel code object and where it came from: compiled by this
+// process's hipRTC, or read from the shipped on-disk cache (lib/jitcache)
+enum JitFrom { kJitCompiled = 0, kJitDisk = 1 };
+struct JitBuild {
+    std::vector<char> code;  // empty: the compile failed (log set)
+    double seconds = 0.0;
+    int from = kJitCompiled;
+};
+
 struct pt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -61,11 +70,12 @@ struct pt_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     // options (pt_set_option)
-    int kernel = -1;       // PT_KERNEL_*; -1 = environment / auto
-    int shade_batch = -1;  // -1 = environment / default
-    int jit = -1;          // 1 use per-scene hipRTC kernels, 0 interpreter; -1 = env (PT_JIT), default 1
-    int jit_bake = -1;     // 0 values from the node table, 1 baked as literals, 2 tier-up; -1 = env (PT_JIT_BAKE), default 2
-    int bin_samples = -1;  // binned pipeline: samples per chunk; -1 = env (PT_BIN_SAMPLES), default 2^29
+    int kernel = PT_KERNEL_AUTO;  // PT_KERNEL_*
+    int shade_batch = 16;         // state-machine kernels: lanes waiting before a shading pass (measured best)
+    int jit = 1;                  // 1 use per-scene hipRTC kernels, 0 interpreter
+    int jit_bake = 2;             // 0 values from the node table, 1 baked as literals, 2 tier-up
+    int bin_samples = 0;          // binned pipeline: samples per chunk; 0 = automatic (bin_samples())
+    size_t bin_auto = 0;          // the automatic chunk size, fixed at the first binned dispatch
     PtJitModule jit_mod;   // scene kernel for the topology (key = its source)
     // tier-up (jit_bake 2): the same kernel with the current values baked in as
     // literals, compiled on a worker thread and used once ready while the
@@ -76,8 +86,9 @@ struct pt_ctx {
     std::string tier_failed;  // a baked source that did not build (not retried)
     // code object (empty: compile failed) and its compile seconds; the worker
     // returns both through the future, so no field is shared with it
-    std::future<std::pair<std::vector<char>, double>> tier_job;
+    std::future<JitBuild> tier_job;
     double tier_seconds = 0.0;
+    int jit_from = -1, tier_from = -1;  // where the loaded builds came from (JitFrom)
     // binned pipeline buffers (pt_binned.h).  A chunk's frames are split over
     // up to kMaxLanes independent pipelines ("lanes"), each on its own stream,
     // so one lane's memory-bound passes (shade, gen, scatter) run beside
@@ -97,9 +108,8 @@ struct pt_ctx {
     size_t bin_cap = 0, ctrl_words = 0;
     hipStream_t xstream[kMaxLanes] = {};   // lanes 1.. streams (created on first use; lane 0 = stream)
     hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {};
-    std::vector<hipEvent_t> order_ev;      // PT_LANE_ORDER: one per (lane, pass) trace launch
-    int bin_lanes = -1;                    // pt_set_option "bin_lanes"; -1 = env PT_BIN_LANES
-    int shade_taps = -1;                   // pt_set_option "shade_taps"; -1 = env PT_SHADE_TAPS
+    int bin_lanes = 2;                     // pt_set_option "bin_lanes" (2: +6 % over 1; 3-4 equal or worse)
+    int shade_taps = 1;                    // pt_set_option "shade_taps": normal taps in the shade pass
     int gen_trace_used = 0;                // the last timed dispatch's first pass made its own camera rays
     int cu_count = 0;
     bool fast_bounds = false;  // every box coordinate inside the reciprocal-division guard
@@ -124,8 +134,8 @@ struct pt_ctx {
 namespace {
 
 // code objects by generated source, shared by every context of the process
-std::map<std::string, std::vector<char>> &jit_cache() {
-    static std::map<std::string, std::vector<char>> cache;
+std::map<std::string, JitBuild> &jit_cache() {
+    static std::map<std::string, JitBuild> cache;
     return cache;
 }
 std::mutex &jit_mutex() {
@@ -133,33 +143,29 @@ std::mutex &jit_mutex() {
     return m;
 }
 
-int jit_bake(const pt_ctx *c) {
-    if (c->jit_bake >= 0) return c->jit_bake;
-    static const int env = [] {
-        const char *v = std::getenv("PT_JIT_BAKE");
-        const int b = v ? std::atoi(v) : 2;
-        return (b >= 0 && b <= 2) ? b : 2;
-    }();
-    return env;
-}
-
 // Code object for a generated source: from the process-wide cache, else
-// compiled (without holding the cache lock).  Empty on failure (log set).
-std::vector<char> jit_code(const std::string &src, std::string &log, double *seconds) {
+// from the on-disk cache or compiled (without holding the cache lock).
+JitBuild jit_code(const std::string &src, std::string &log) {
+    JitBuild b;
     {
         std::lock_guard<std::mutex> g(jit_mutex());
         auto it = jit_cache().find(src);
-        if (it != jit_cache().end()) return it->second;
+        if (it != jit_cache().end()) {
+            b = it->second;
+            b.seconds = 0.0;
+            return b;
+        }
     }
     const auto t0 = std::chrono::steady_clock::now();
-    std::vector<char> code;
-    if (!pt_jit_compile_source(src, code, log)) code.clear();
-    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (!code.empty()) {
+    bool disk = false;
+    if (!pt_jit_compile_source(src, b.code, log, &disk)) b.code.clear();
+    b.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    b.from = disk ? kJitDisk : kJitCompiled;
+    if (!b.code.empty()) {
         std::lock_guard<std::mutex> g(jit_mutex());
-        jit_cache()[src] = code;
+        jit_cache()[src] = b;
     }
-    return code;
+    return b;
 }
 
 // Install a finished tier-up compile if it is still the one the current
@@ -168,14 +174,14 @@ std::vector<char> jit_code(const std::string &src, std::string &log, double *sec
 void jit_tier_poll(pt_ctx *c, bool wait) {
     if (c->tier_job.valid() &&
         (wait || c->tier_job.wait_for(std::chrono::seconds(0)) == std::future_status::ready)) {
-        auto done = c->tier_job.get();
-        std::vector<char> &code = done.first;
-        c->tier_seconds = done.second;
-        if (code.empty()) c->tier_failed = c->tier_job_src;
-        if (!code.empty() && c->tier_job_src == c->tier_want && !c->jit_tier.module) {
+        JitBuild done = c->tier_job.get();
+        c->tier_seconds = done.seconds;
+        if (done.code.empty()) c->tier_failed = c->tier_job_src;
+        if (!done.code.empty() && c->tier_job_src == c->tier_want && !c->jit_tier.module) {
             std::string err;
-            if (pt_jit_load(code, c->jit_tier, err)) {
+            if (pt_jit_load(done.code, c->jit_tier, err)) {
                 c->jit_tier.key = c->tier_job_src;
+                c->tier_from = done.from;
             } else {
                 c->jit_log = err;
                 c->tier_failed = c->tier_job_src;
@@ -189,9 +195,7 @@ void jit_tier_poll(pt_ctx *c, bool wait) {
         c->tier_job_src = src;
         c->tier_job = std::async(std::launch::async, [src]() {
             std::string log;
-            double secs = 0.0;
-            std::vector<char> code = jit_code(src, log, &secs);
-            return std::make_pair(std::move(code), secs);
+            return jit_code(src, log);
         });
         if (wait) jit_tier_poll(c, true);
     }
@@ -203,25 +207,17 @@ const PtJitModule *jit_active(const pt_ctx *c) {
     return c->jit_mod.module ? &c->jit_mod : nullptr;
 }
 
-bool jit_wanted(const pt_ctx *c) {
-    if (c->jit >= 0) return c->jit != 0;
-    static const int env = [] {
-        const char *v = std::getenv("PT_JIT");
-        return v ? std::atoi(v) : 1;
-    }();
-    return env != 0;
-}
 
 // (Re)build the scene-specialised kernel when the generated source changed.
 // A failure leaves the interpreter kernel in use and records the log.
 void jit_refresh(pt_ctx *c, const std::vector<PtNode> &nodes, const std::vector<PtAabb> &boxes) {
-    if (!jit_wanted(c)) {
+    if (!c->jit) {
         pt_jit_unload(c->jit_mod);
         pt_jit_unload(c->jit_tier);
         c->tier_want.clear();
         return;
     }
-    const int bake = jit_bake(c);
+    const int bake = c->jit_bake;
     std::string src = pt_jit_source(nodes, boxes, c->fast_bounds, bake == 1);
     // the tier-up build for these values (jit_bake 2); a stale one is dropped
     c->tier_want = bake == 2 ? pt_jit_source(nodes, boxes, c->fast_bounds, true) : std::string();
@@ -229,17 +225,19 @@ void jit_refresh(pt_ctx *c, const std::vector<PtNode> &nodes, const std::vector<
     if (!(c->jit_mod.module && c->jit_mod.key == src)) {
         pt_jit_unload(c->jit_mod);
         std::string log;
-        std::vector<char> code = jit_code(src, log, &c->jit_seconds);
-        if (code.empty()) {
+        JitBuild b = jit_code(src, log);
+        c->jit_seconds = b.seconds;
+        if (b.code.empty()) {
             c->jit_log = "hipRTC compile failed: " + log;
             return;
         }
         std::string err;
-        if (!pt_jit_load(code, c->jit_mod, err)) {
+        if (!pt_jit_load(b.code, c->jit_mod, err)) {
             c->jit_log = err;
             return;
         }
         c->jit_mod.key = std::move(src);
+        c->jit_from = b.from;
         c->jit_log.clear();
     }
     if (bake == 2) jit_tier_poll(c, false);
@@ -631,48 +629,30 @@ static size_t bin_bytes_per_sample(const pt_ctx *c) {
     return kBinBytesPerSample + (c->n_check > 64 ? kBinBytesWide : 0);
 }
 
+// Samples per chunk: pt_set_option "bin_samples", else automatic: 2^29 (a
+// whole 256-spp 1080p render: 82 GB of HBM at 152 B per sample; every pass's
+// tail is paid once per chunk, so larger chunks are faster: 64 -> 256 frames
+// per chunk +5 %), at most half of what this context could hold on its
+// device -- the free memory plus the chunk buffers it already owns (other
+// contexts' allocations count as used, so several ranks sharing one GPU each
+// size to what is left).  The automatic size is fixed at the context's first
+// binned dispatch, so a workload chunks the same way on every later one
+// whatever other allocations come and go.  The caller's current device is
+// left as it was.
 static size_t bin_samples(pt_ctx *c) {
     if (c->bin_samples > 0) return size_t(c->bin_samples);
-    static const long env = [] {
-        const char *v = std::getenv("PT_BIN_SAMPLES");
-        return v ? std::atol(v) : 0L;
-    }();
-    if (env >= 64) return size_t(env);
-    // default: 2^29 samples (a whole 256-spp 1080p render: 82 GB of HBM at
-    // 152 B per sample; every pass's tail is paid once per chunk, so larger
-    // chunks are faster: 64 -> 256 frames per chunk +5 %), at most half of
-    // what this context could hold on its device: the free memory plus the
-    // chunk buffers it already owns (other contexts' allocations count as
-    // used, so several ranks sharing one GPU each size to what is left)
+    if (c->bin_auto) return c->bin_auto;
     const size_t per = bin_bytes_per_sample(c);
     size_t free_b = 0, total_b = 0;
-    if (hipSetDevice(c->device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess || total_b == 0)
-        return size_t(1) << 27;
+    int prev = -1;
+    const bool have_prev = hipGetDevice(&prev) == hipSuccess;
+    const bool ok = hipSetDevice(c->device) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+                    total_b != 0;
+    if (have_prev) (void)hipSetDevice(prev);
+    if (!ok) return size_t(1) << 27;
     const size_t held = c->bin_cap * size_t(c->n_lanes) * per;
     const size_t cap = std::max<size_t>(size_t(1) << 20, (free_b + held) / 2 / per);
     return std::min<size_t>(size_t(1) << 29, cap);
-}
-
-// Pipelines per chunk (1..kMaxLanes): pt_set_option "bin_lanes", else env PT_BIN_LANES.
-static int bin_lanes(const pt_ctx *c) {
-    if (c->bin_lanes >= 1 && c->bin_lanes <= pt_ctx::kMaxLanes) return c->bin_lanes;
-    static const int env = [] {
-        const char *v = std::getenv("PT_BIN_LANES");
-        const int n = v ? std::atoi(v) : 2;
-        return (n >= 1 && n <= pt_ctx::kMaxLanes) ? n : 2;
-    }();
-    return env;
-}
-
-// Normal taps in the shade pass (scene kernels only): pt_set_option
-// "shade_taps", else env PT_SHADE_TAPS.
-static bool shade_taps(const pt_ctx *c) {
-    if (c->shade_taps >= 0) return c->shade_taps != 0;
-    static const int env = [] {
-        const char *v = std::getenv("PT_SHADE_TAPS");
-        return v ? std::atoi(v) : 1;
-    }();
-    return env != 0;
 }
 
 static void free_bin(pt_ctx *c) {
@@ -733,7 +713,7 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
     }
     for (int i = 0; i < lanes; ++i) {
         HIPCHK(c, hipMemsetAsync(c->lane[i].hist, 0, PT_BINS * sizeof(uint32_t), c->stream));
-        HIPCHK(c, hipMemsetAsync(c->lane[i].ctrl, 0, words * sizeof(uint32_t), c->stream));  // (fused-scan tickets)
+        HIPCHK(c, hipMemsetAsync(c->lane[i].ctrl, 0, words * sizeof(uint32_t), c->stream));
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->n_lanes = lanes;
@@ -777,9 +757,10 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         lc0 = int32_t(uint32_t(lc0) + spp - 1);
         spp = 1;
     }
+    if (!c->bin_samples && !c->bin_auto) c->bin_auto = bin_samples(c);  // (fixed from now on)
     const uint32_t F = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, bin_samples(c) / n_pix)));
     const int passes = L.bounces + 1;
-    const int lanes = int(std::min<uint32_t>(uint32_t(bin_lanes(c)), F));
+    const int lanes = int(std::min<uint32_t>(uint32_t(c->bin_lanes), F));
     const uint32_t FL = (F + uint32_t(lanes) - 1) / uint32_t(lanes);  // frames per lane
     int rc = ensure_bin(c, size_t(n_pix) * FL, size_t(passes), lanes);
     if (rc != PT_OK) return rc;
@@ -787,63 +768,45 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     auto item_grid = [&](size_t n) {
         return unsigned(std::max<size_t>(1, std::min<size_t>((n + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK, 4 * cu)));
     };
+    // scatter: 4 blocks per CU (8 / 16 measured equal), each one contiguous
+    // run of PT_SCATTER_ITEMS-slot tiles
     auto scatter_grid = [&](size_t n) {
         const size_t tile = PT_BIN_BLOCK * PT_SCATTER_ITEMS;
-        static const size_t per_cu = [] {
-            const char *e = std::getenv("PT_SCATTER_GRID");
-            return size_t(e && std::atoi(e) > 0 ? std::atoi(e) : 4);
-        }();
-        return unsigned(std::max<size_t>(1, std::min<size_t>((n + tile - 1) / tile, per_cu * cu)));
+        return unsigned(std::max<size_t>(1, std::min<size_t>((n + tile - 1) / tile, size_t(4) * cu)));
     };
     const PtJitModule *jm = jit_active(c);
     const bool jit = jm != nullptr;
     // normal taps in the shade pass: march-only trace + tapping shade (scene kernels)
-    const bool taps_shade = jit && shade_taps(c);
+    const bool taps_shade = jit && c->shade_taps;
     hipFunction_t jf = jit ? (taps_shade ? (stats ? jm->trace_m_stats : jm->trace_m)
                                          : (stats ? jm->trace_stats : jm->trace))
                            : nullptr;
     int per_cu = 0;
     if (jit) HIPCHK(c, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jf, 64, 0));
     else per_cu = pt_bin_trace_blocks_per_cu(stats);
-    static const int trace_cu_env = [] {  // A/B knob: trace blocks (waves) per CU, below the occupancy limit
-        const char *v = std::getenv("PT_TRACE_BLOCKS");
-        return v ? std::atoi(v) : 0;
-    }();
-    if (trace_cu_env > 0 && trace_cu_env < per_cu) per_cu = trace_cu_env;
-    // default: leave one wave slot per SIMD (4 per CU) to the other pipeline,
-    // so its shade / scatter / scan blocks run beside the persistent trace
-    // waves instead of waiting for a pass to drain: 28 of 32 with the 64-VGPR
+    // leave one wave slot per SIMD (4 per CU) to the other pipeline, so its
+    // shade / scatter / scan blocks run beside the persistent trace waves
+    // instead of waiting for a pass to drain: 28 of 32 with the 64-VGPR
     // (8-wave) build (+1.5 % over 24 of 28 at 72 VGPRs), 24 of 28 with the
     // 72-VGPR fallback (+1.5 % over 28 of 28)
-    else if (trace_cu_env == 0 && per_cu > 8) per_cu = std::min(per_cu - 4, 28);
+    if (per_cu > 8) per_cu = std::min(per_cu - 4, 28);
     const unsigned trace_grid = cu * unsigned(std::max(1, per_cu));
     // the first pass's kernel may have been rebuilt at 7 waves on its own
     // (pt_jit_compile_source): the same one-slot-per-SIMD rule on its occupancy
     unsigned trace_g_grid = trace_grid;
-    if (jit && jm->trace_g && trace_cu_env == 0) {
+    if (jit && jm->trace_g) {
         int g = 0;
         HIPCHK(c, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&g, jm->trace_g, 64, 0));
         if (g > 8) g = std::min(g - 4, 28);
         if (g > 0 && g < per_cu) trace_g_grid = cu * unsigned(g);
     }
-    static const int run_max = [] {  // A/B knob
-        const char *v = std::getenv("PT_BIN_RUN");
-        const int r = v ? std::atoi(v) : 512;
-        return r >= 64 ? (r / 64) * 64 : 256;
-    }();
-    static const int refill_min = [] {  // A/B knob
-        const char *v = std::getenv("PT_REFILL_MIN");
-        const int r = v ? std::atoi(v) : 2;
-        return r >= 1 && r <= 64 ? r : 4;
-    }();
-    static const unsigned shade_cu_env = [] {  // A/B knob: shade blocks per CU
-        const char *v = std::getenv("PT_SHADE_BLOCKS");
-        return v ? unsigned(std::atoi(v)) : 0u;
-    }();
-    // default: two rounds of the tapping shade kernel's 7 resident blocks per
-    // CU (measured +2 % over 8, whose last round ran on a quarter of the
-    // chip); 8 for the table kernel
-    const unsigned shade_cu = shade_cu_env ? shade_cu_env : (taps_shade ? 14u : 8u);
+    // trace runs of at most 512 rays (256 / 768 / 1024 equal, 128 -7 %), a
+    // refill once 2 lanes are free (1 / 4 equal)
+    constexpr int run_max = 512, refill_min = 2;
+    // two rounds of the tapping shade kernel's 7 resident blocks per CU
+    // (measured +2 % over 8, whose last round ran on a quarter of the chip;
+    // 8 / 16 at 8 waves -0.3 %); 8 for the table kernel
+    const unsigned shade_cu = taps_shade ? 14u : 8u;
     const unsigned shade_grid =
         unsigned(std::max<size_t>(1, std::min<size_t>((c->bin_cap + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK, size_t(shade_cu) * cu)));
 
@@ -890,16 +853,11 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             for (int i = 1; i < nl; ++i) HIPCHK(c, hipStreamWaitEvent(c->lane[i].stream, c->fork_ev, 0));
         }
         // the first pass takes the primary rays in generation order (gen lists
-        // them, the host sets the count; no histogram, scan or scatter: +1 %);
-        // PT_GEN_BIN=1 bins them like every other pass
-        static const int gen_bin = [] {
-            const char *v = std::getenv("PT_GEN_BIN");
-            return v ? std::atoi(v) : 0;
-        }();
-        // (only when every local tile lies inside the image: then every
-        // generated slot is live and the list is the identity order)
+        // them, the host sets the count; no histogram, scan or scatter: +1 %)
+        // -- only when every local tile lies inside the image: then every
+        // generated slot is live and the list is the identity order
         const bool full_tiles = L.width % PT_TILE == 0 && L.height % PT_TILE == 0 && L.debug == 0;
-        for (int i = 0; i < nl && !gen_bin && full_tiles; ++i) {
+        for (int i = 0; i < nl && full_tiles; ++i) {
             P[i].gen_order = 1;
             // pass 0's control words = {count, run cursors 0}: stream-ordered
             // fills, no host buffer whose lifetime the copy would have to outlast
@@ -908,22 +866,15 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             HIPCHK(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->lane[i].ctrl), int(P[i].n_src_const), 1,
                                         c->lane[i].stream));
         }
-        static const int gen_jit = [] {  // A/B knob: PT_GEN_JIT=0 keeps the ahead-of-time gen kernel
-            const char *v = std::getenv("PT_GEN_JIT");
-            return v ? std::atoi(v) : 1;
-        }();
         // no gen pass: the first trace pass makes its windows' camera rays
-        // itself (scene kernels, generation order; PT_GEN_TRACE=0 keeps gen)
-        static const int gen_trace = [] {
-            const char *v = std::getenv("PT_GEN_TRACE");
-            return v ? std::atoi(v) : 1;
-        }();
+        // itself (scene kernels, generation order: +2.8 %); otherwise the
+        // scene's gen kernel (straight-line bounds(): +1.4 % over the AOT one)
         if (!stats) c->gen_trace_used = 0;
         for (int i = 0; i < nl; ++i) {
-            if (gen_trace && P[i].gen_order && jit && taps_shade && !stats && jm->trace_g) {
+            if (P[i].gen_order && jit && taps_shade && !stats && jm->trace_g) {
                 P[i].gen_trace = 1;
                 c->gen_trace_used = 1;
-            } else if (jit && gen_jit) {
+            } else if (jit) {
                 void *args[] = {&P[i]};
                 HIPCHK(c, hipModuleLaunchKernel(stats ? jm->gen_stats : jm->gen, item_grid(size_t(P[i].n_src_const)), 1,
                                                 1, PT_BIN_BLOCK, 1, 1, 0, c->lane[i].stream, args, nullptr));
@@ -932,14 +883,6 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 HIPCHK(c, hipGetLastError());
             }
         }
-        // PT_FUSED_SCAN=1: the next pass's histogram scan in the shade
-        // pass's last block (bin_scan_fused) instead of a one-wave launch.
-        // Equal within box noise on C2 and C3 (`DESIGN.md` 8b), so the
-        // kernel boundary, whose ordering needs no argument, stays the default.
-        static const int fused_scan = [] {
-            const char *v = std::getenv("PT_FUSED_SCAN");
-            return v ? std::atoi(v) : 0;
-        }();
         // shade the hits trace pass k wrote into ray[(k + 1) & 1]: ended paths
         // store their colour, the rest get their next ray, bounds() and bin
         auto shade = [&](int i, int k) -> int {
@@ -947,8 +890,6 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             S.bounce = k;
             S.rin = c->lane[i].ray[(k + 1) & 1];
             S.n_src = c->lane[i].ctrl + size_t(PT_CTRL_STRIDE) * k;
-            // the next pass's histogram scan in the shade pass's last block
-            S.scan_ctrl = (fused_scan && k + 1 < passes) ? c->lane[i].ctrl + size_t(PT_CTRL_STRIDE) * (k + 1) : nullptr;
             if (!stats) HIPCHK(c, record_event(c->slog, c->lane[i].stream));
             if (taps_shade) {
                 void *args[] = {&S};
@@ -961,24 +902,6 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             if (!stats) HIPCHK(c, record_event(c->slog, c->lane[i].stream));
             return PT_OK;
         };
-        // A/B knob PT_LANE_ORDER: the lanes' trace launches ordered by events.
-        // 1: lane i's first trace pass starts after lane i-1's has ended
-        // (staggered start); 2: the trace passes alternate, lane i's pass k
-        // after lane i-1's pass k and lane 0's pass k after the last lane's
-        // pass k-1 (a lane's shade and scatter run beside the next lane's trace)
-        static const int lane_order = [] {
-            const char *v = std::getenv("PT_LANE_ORDER");
-            return v ? std::atoi(v) : 0;
-        }();
-        const bool ordered = lane_order != 0 && nl > 1;
-        if (ordered) {
-            while (c->order_ev.size() < size_t(nl) * size_t(passes)) {
-                hipEvent_t e;
-                HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-                c->order_ev.push_back(e);
-            }
-        }
-        auto order_ev = [&](int i, int k) { return c->order_ev[size_t(k) * size_t(nl) + size_t(i)]; };
         for (int k = 0; k < passes; ++k) {
             for (int i = 0; i < nl; ++i) {
                 // pass k: bin the rays of ray[k & 1] (gen's, or the shaded hits of pass k-1), trace them into the other
@@ -993,16 +916,10 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 p.ctrl = l.ctrl + size_t(PT_CTRL_STRIDE) * k;
                 p.n_src = k == 0 ? nullptr : l.ctrl + size_t(PT_CTRL_STRIDE) * (k - 1);
                 if (k > 0 || !p.gen_order) {
-                    if (k == 0 || !fused_scan) pt_launch_bin(PtBinStage::Scan, p, stats, 1, l.stream);
+                    pt_launch_bin(PtBinStage::Scan, p, stats, 1, l.stream);
                     pt_launch_bin(PtBinStage::Scatter, p, stats, scatter_grid(k == 0 ? p.n_src_const : c->bin_cap),
                                   l.stream);
                     HIPCHK(c, hipGetLastError());
-                }
-                if (ordered) {
-                    if (lane_order == 1 && k == 0 && i > 0)
-                        HIPCHK(c, hipStreamWaitEvent(l.stream, order_ev(i - 1, 0), 0));
-                    else if (lane_order == 2 && (i > 0 || k > 0))
-                        HIPCHK(c, hipStreamWaitEvent(l.stream, i > 0 ? order_ev(i - 1, k) : order_ev(nl - 1, k - 1), 0));
                 }
                 if (!stats) HIPCHK(c, record_event(c->tlog, l.stream));
                 if (jit) {
@@ -1015,7 +932,6 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                     HIPCHK(c, hipGetLastError());
                 }
                 if (!stats) HIPCHK(c, record_event(c->tlog, l.stream));
-                if (ordered) HIPCHK(c, hipEventRecord(order_ev(i, k), l.stream));
             }
         }
         for (int i = 0; i < nl; ++i)  // the last bounce's hits end their paths
@@ -1083,20 +999,7 @@ static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, u
     L.fov = s->fov;
     L.aspect = k->aspect;
     L.write = 1;
-    // tuning knobs (A/B experiments; defaults are the shipped configuration)
-    static const int env_kernel = [] {
-        const char *v = std::getenv("PT_KERNEL");
-        if (!v) return PT_KERNEL_AUTO;
-        if (!std::strcmp(v, "simple")) return PT_KERNEL_SIMPLE;
-        if (!std::strcmp(v, "wave")) return PT_KERNEL_WAVEFRONT;
-        if (!std::strcmp(v, "binned")) return PT_KERNEL_BINNED;
-        return PT_KERNEL_AUTO;
-    }();
-    static const int env_batch = [] {
-        const char *v = std::getenv("PT_SHADE_BATCH");
-        return v ? std::atoi(v) : 0;
-    }();
-    L.kernel = c->kernel >= 0 ? c->kernel : env_kernel;
+    L.kernel = c->kernel;
     if (L.kernel == PT_KERNEL_AUTO) {
         // small dispatches take the tile-resident wave kernel: one launch, no
         // pass sequence and no per-pass tails.  Crossover measured at about
@@ -1105,7 +1008,7 @@ static int make_launch(pt_ctx *c, const pt_constants *k, const pt_settings *s, u
         const double work = double(L.n_tiles) * 64.0 * double(spp) * double(std::max<size_t>(1, c->ops.size()));
         L.kernel = work < 134217728.0 ? PT_KERNEL_WAVEFRONT : PT_KERNEL_BINNED;
     }
-    L.shade_batch = c->shade_batch > 0 ? c->shade_batch : (env_batch > 0 ? env_batch : 16);  // measured best
+    L.shade_batch = c->shade_batch;
     return PT_OK;
 }
 
@@ -1237,6 +1140,16 @@ int pt_comm_init(pt_ctx *c, uint32_t nranks, uint32_t rank, const uint8_t id[PT_
     return PT_OK;
 }
 
+int pt_comm_size(pt_ctx *c, uint32_t *nranks) {
+    if (!c || !nranks) return PT_ERR_INVALID;
+    if (!c->comm) return fail(c, PT_ERR_STATE, "pt_comm_init not called");
+    int n = 0;
+    ncclResult_t r = ncclCommCount(c->comm, &n);
+    if (r != ncclSuccess) return fail(c, PT_ERR_RCCL, std::string("ncclCommCount: ") + ncclGetErrorString(r));
+    *nranks = uint32_t(n);
+    return PT_OK;
+}
+
 int pt_reduce_accum(pt_ctx *c, int root) {
     if (!c) return PT_ERR_INVALID;
     if (!c->comm) return fail(c, PT_ERR_STATE, "pt_comm_init not called");
@@ -1357,8 +1270,13 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "trace_ms")) HIPCHK(c, event_log_ms(c->tlog, value));  // summed over the trace passes
     else if (!std::strcmp(key, "shade_ms")) HIPCHK(c, event_log_ms(c->slog, value));  // summed over the shade passes
     else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * double(c->n_lanes) * double(bin_bytes_per_sample(c));
-    else if (!std::strcmp(key, "bin_lanes")) *value = double(bin_lanes(c));
-    else if (!std::strcmp(key, "shade_taps")) *value = shade_taps(c) ? 1.0 : 0.0;
+    else if (!std::strcmp(key, "bin_lanes")) *value = double(c->bin_lanes);
+    else if (!std::strcmp(key, "shade_taps")) *value = c->shade_taps ? 1.0 : 0.0;
+    else if (!std::strcmp(key, "jit_cache")) {
+        // where the scene kernel in use came from: 1 the shipped on-disk cache
+        // (lib/jitcache), 0 this process's hipRTC, -1 none loaded
+        *value = c->jit_tier.module ? c->tier_from : (c->jit_mod.module ? c->jit_from : -1);
+    }
     else if (!std::strcmp(key, "gen_trace")) *value = double(c->gen_trace_used);
     else if (!std::strncmp(key, "tap_stat_", 9)) {  // tap_stat_<k>: counter k of the last stats run's shade-pass taps
         const int k = std::atoi(key + 9);
@@ -1393,7 +1311,6 @@ void pt_destroy(pt_ctx *c) {
         if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
     }
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
-    for (hipEvent_t e : c->order_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (hipEvent_t e : c->tlog.ev) (void)hipEventDestroy(e);

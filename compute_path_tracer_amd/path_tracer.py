@@ -202,6 +202,12 @@ class PathTracer:
         buf = (ctypes.c_uint8 * N.PT_COMM_ID_BYTES).from_buffer_copy(uid)
         self._chk("pt_comm_init", self._L.pt_comm_init(self._ctx, nranks, rank, buf))
 
+    def comm_size(self) -> int:
+        """Ranks of the context's RCCL communicator (ncclCommCount)."""
+        n = ctypes.c_uint32()
+        self._chk("pt_comm_size", self._L.pt_comm_size(self._ctx, ctypes.byref(n)))
+        return int(n.value)
+
     def reduce(self, root: int = 0) -> None:
         self._chk("pt_reduce_accum", self._L.pt_reduce_accum(self._ctx, root))
 

@@ -195,6 +195,10 @@ int pt_get_size(const pt_ctx *ctx, uint32_t *width, uint32_t *height);
 #define PT_COMM_ID_BYTES 128
 int pt_comm_get_unique_id(uint8_t id[PT_COMM_ID_BYTES]);
 int pt_comm_init(pt_ctx *ctx, uint32_t nranks, uint32_t rank, const uint8_t id[PT_COMM_ID_BYTES]);
+/* Ranks of the context's communicator as RCCL reports them (ncclCommCount):
+ * the check that an N-GPU run reduced over N ranks.  PT_ERR_STATE before
+ * pt_comm_init. */
+int pt_comm_size(pt_ctx *ctx, uint32_t *nranks);
 /* Sum of every rank's image into this context's result image on `root`
  * (out of place: the local accumulation keeps progressing). */
 int pt_reduce_accum(pt_ctx *ctx, int root);

@@ -11,7 +11,8 @@ if w.get("xform_shape"):
     cull = {"lane_culled": round(w["culled"] / w["xform_shape"], 4),
             "wave_evals_per_shape": round(w["wave_evals"] / max(1, w["wave_shapes"]), 4),
             "wave_evals_per_map": round(w["wave_evals"] / max(1, w["wave_maps"]), 3)}
-sh = d["roofline"].get("shade", {})
-print(d["value"], d["roofline"]["kernel_ms_per_launch"], "shade_ms_step", sh.get("ms_per_step_summed"),
-      "trace_ms_step", round(d["roofline"]["kernel_ms_per_launch"] * d["roofline"]["kernel_launches_per_step"], 3),
+r = d["roofline"]
+sh, eq = r.get("shade", {}), r.get("reference_equivalent", {})
+print(d["value"], "trace_ms_launch", eq.get("trace_ms_per_launch"), "shade_ms_launch", eq.get("shade_ms_per_launch"),
+      "solo trace/shade ms", r["kernel_ms_per_launch"], sh.get("ms_per_launch"), "frac", r["frac"], sh.get("frac"),
       json.dumps(d.get("schedule", {})), json.dumps(cull))

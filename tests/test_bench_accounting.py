@@ -63,3 +63,35 @@ def test_hw_view_and_cpu_info():
     info = bench.cpu_info()
     assert info["os_cpu_count"] >= 1 and info["affinity"] >= 1 and info["model"]
     assert 1 <= bench.default_cpu_threads() <= info["affinity"]
+    assert bench.default_cpu_threads() == info["affinity"]  # every CPU: the oracle is pthreads, not OpenMP
+
+
+def test_resolve_world():
+    """--gpus N without a launcher starts N ranks; under a launcher it must
+    agree with WORLD_SIZE (a silent 1-GPU run claimed N)."""
+    assert bench.resolve_world(None, {}) == (1, False)
+    assert bench.resolve_world(1, {}) == (1, False)
+    assert bench.resolve_world(8, {}) == (8, True)
+    assert bench.resolve_world(None, {"WORLD_SIZE": "4"}) == (4, False)
+    assert bench.resolve_world(4, {"WORLD_SIZE": "4"}) == (4, False)
+    with pytest.raises(SystemExit):
+        bench.resolve_world(8, {"WORLD_SIZE": "2"})
+    with pytest.raises(SystemExit):
+        bench.resolve_world(0, {})
+    cmd = bench.launcher_cmd(["--gpus", "8", "--steps", "3"], 8, 29501)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=8" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and cmd[-3:] == ["--gpus", "8", "--steps", "3"][-3:]
+
+
+def test_gpus_mismatch_exits_before_the_gpu():
+    """A launcher's WORLD_SIZE that disagrees with --gpus ends bench.py with a
+    non-zero status before it imports the library or touches a GPU."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "8"], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr and not any(l.startswith("{") for l in r.stdout.splitlines())

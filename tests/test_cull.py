@@ -347,7 +347,7 @@ def test_jit_disk_cache_round_trip(tmp_path):
         f.seek(-100, 2)
         f.write(b"\xff" * 8)
     assert _probe("c1", "1", PT_JIT_CACHE="1", PT_JIT_CACHE_DIR=d)[1] == size
-    _probe("c1", "1", PT_JIT_CACHE="2", PT_JIT_CACHE_DIR=d, PT_JIT_SHADE_SPILL_OK="17")
+    _probe("c1", "1", PT_JIT_CACHE="2", PT_JIT_CACHE_DIR=d, PT_JIT_DEFS="PT_UNUSED_PROBE")
     assert len(os.listdir(d)) == 2
 
 

@@ -61,3 +61,22 @@ def test_two_ranks_strong_config4_leg(gpu):
     assert leg["scaling"] == "strong" and leg["n_gpus"] == 2
     assert leg["config"]["width"] == 3840 and leg["config"]["spp_per_step"] == 256
     assert leg["value"] > 0 and leg["reduce_ms"] > 0
+
+
+@pytest.mark.timeout(600)
+def test_bench_gpus_flag_launches_the_ranks(gpu):
+    """`bench.py --gpus 2` with no launcher starts the two ranks itself
+    (torch.distributed.run as a child process) and the line says so: n_gpus
+    2, the tile split bit-exact against a one-context render (VERDICT r03:
+    --gpus was parsed and ignored)."""
+    cmd = [sys.executable, "-u", "bench.py", "--gpus", "2", "--no-cpu-baseline", "--dist-backend", "gloo",
+           "--width", "480", "--height", "272", "--spp", "4", "--steps", "2", "--warmup", "1", "--validate"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PT_BENCH_SHARE_GPU="1", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=500)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["validation"]["bit_exact"] is True
+    assert out["rccl_ranks"] is None  # (gloo host reduce: RCCL refuses two ranks on one device)

@@ -387,12 +387,16 @@ def test_rccl_single_rank_reduce_and_errors(gpu):
     with pytest.raises(N.NativeError) as e:
         pt.read_reduced()
     assert e.value.code == N.PT_ERR_STATE
+    with pytest.raises(N.NativeError) as e:
+        pt.comm_size()
+    assert e.value.code == N.PT_ERR_STATE
     uid = PathTracer.comm_unique_id()
     assert len(uid) == N.PT_COMM_ID_BYTES
     with pytest.raises(N.NativeError) as e:
         pt.comm_init(1, 1, uid)  # rank >= nranks
     assert e.value.code == N.PT_ERR_INVALID
     pt.comm_init(1, 0, uid)
+    assert pt.comm_size() == 1  # (ncclCommCount: what bench.py reports as rccl_ranks)
     for root in (-1, 1):
         with pytest.raises(N.NativeError) as e:
             pt.reduce(root)
