@@ -118,18 +118,19 @@ def pipeline_bytes(st: dict, pixels: float, gen_trace: bool = False) -> dict:
     (pt_binned.h), from the instrumented run's counters: S samples, G
     segments (rays entering a trace pass), H shaded hits.  Misses G - H end
     in the trace pass; G - S rays continue from a shade pass; H - (G - S)
-    paths end there.  Records are 64 B (PtRay).
+    paths end there.  Rays are 64 B records (PtRay), hit quads 16 B.
     - gen writes each sample's ray and zeroes its colour slot (64 + 16 B)
       and lists it (4 B) -- or, gen_trace (the bench default), there is no
-      gen pass: the first trace pass makes its rays, and each sample's
-      colour slot is written once in pass 0 (16 B: by the trace pass at a
-      miss, by the shade pass at a hit);
+      gen pass: the first trace pass makes its rays and stores them at their
+      slots (64 B), and each sample's colour slot is written once in pass 0
+      (16 B: by the trace pass at a miss, by the shade pass at a hit);
     - scatter reads every later slot's 4 B key and writes a 4 B binned slot
       (the first pass takes generation order);
     - trace reads a slot (4 B) and its ray (64 B) (not in the first pass
-      with gen_trace) and writes a hit record (64 B) or a miss marker (16 B);
-    - shade reads each hit's record (64 B) and each miss's marker (16 B) and
-      writes the next ray + key (64 + 4 B) or a NONE key (4 B);
+      with gen_trace) and writes one 16 B hit quad per ray, hit or miss;
+    - shade reads each traced ray's quad (16 B) and each hit's ray (64 B,
+      gathered by slot) and writes the next ray + key (64 + 4 B) or a NONE
+      key (4 B);
     - fold reads each frame's colour (16 B) and reads + writes the texel
       (32 B per pixel).
     Not counted: the colour slot's read-modify-write at emitting hits after
@@ -141,12 +142,15 @@ def pipeline_bytes(st: dict, pixels: float, gen_trace: bool = False) -> dict:
     traced_in = G - S if gen_trace else G
     parts = {"gen": 0.0 if gen_trace else 84.0 * S,
              "scatter": 8.0 * cont,
-             "trace": 68.0 * traced_in + 64.0 * H + 16.0 * miss,
-             "shade": 64.0 * H + 16.0 * miss + 68.0 * cont + 4.0 * (ended + miss),
+             "trace": 68.0 * traced_in + 16.0 * G + (64.0 * S if gen_trace else 0.0),
+             "shade": 16.0 * G + 64.0 * H + 68.0 * cont + 4.0 * (ended + miss),
              "fold": 16.0 * S + 32.0 * pixels}
     if gen_trace:
         parts["colour0"] = 16.0 * S
     parts["total"] = sum(parts.values())
+    # per trace kernel: the march-only passes (bounces 1..) and the first pass
+    parts["trace_m"] = (68.0 + 16.0) * (G - S)
+    parts["trace_first"] = parts["trace"] - parts["trace_m"]
     return parts
 
 
@@ -182,8 +186,10 @@ def schedule_metrics(st_all: dict, taps: dict) -> dict:
 
 def profiled(config: dict):
     """The newest committed rocprofv3 PMC summary (profiles/*_pmc.json,
-    scripts/summarize_profile.py) taken on this same workload, as (summary,
-    path); None if there is none."""
+    scripts/summarize_profile.py) of this same workload with per-kernel
+    figures, taken with ONE pipeline (bench.py --pipelines 1: each kernel's
+    counters are its own, as roofline.frac's times are), as (summary, path);
+    None if there is none."""
     import glob
 
     best = None
@@ -193,10 +199,8 @@ def profiled(config: dict):
         except (OSError, ValueError):
             continue
         cfg = d.get("bench_config") or {}
-        keys = ("width", "height", "bounces", "spp_per_step")
-        same_lanes = cfg.get("pipelines", 2) == config.get("pipelines", 2)  # (older summaries: the default 2)
-        if all(cfg.get(k) == config.get(k) for k in keys) and cfg.get("workload") == config.get("workload") \
-                and same_lanes and d.get("derived", {}).get("hbm_bytes_per_launch"):
+        keys = ("width", "height", "bounces", "spp_per_step", "workload")
+        if all(cfg.get(k) == config.get(k) for k in keys) and cfg.get("pipelines") == 1 and d.get("per_kernel"):
             best = (d, os.path.relpath(f, ROOT))
     return best
 
@@ -615,6 +619,14 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
                         "(their launches' event times overlap)",
               "flops": "algorithmic: every counted event at its SURVEY 8(d) weight, culled evaluations included "
                        "(what the reference's loop would execute)"}
+        # executed flops over the timed steps' overlapped launch times: the
+        # kernels share the GPU there, so their fractions of one peak must
+        # sum to <= 1 (the algorithmic view above does not: culled work)
+        ov_t, ov_s = executed_split(st, taps, n_aabb, gen_trace)
+        ov = {"trace_frac": round(ov_t / (t_ms * 1e-3) / 1e12 / PEAK_F32_TFLOPS, 4),
+              "shade_frac": round(ov_s / (s_ms * 1e-3) / 1e12 / PEAK_F32_TFLOPS, 4), "timing": eq["timing"],
+              "flops": "executed (as roofline.flops)"}
+        ov["sum"] = round(ov["trace_frac"] + ov["shade_frac"], 4)
         # executed flops over each kernel's own time: the one-pipeline run
         # (solo_pipeline) when there is one, else the timed steps
         if solo is not None:
@@ -689,7 +701,7 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
                          "of the metric are the image's 32 B per pixel per dispatch (image_gbs)",
                 "algorithmic_bytes_per_dispatch": pipe["total"],
                 "bytes_per_sample": round(pipe["total"] / max(1, st["samples"]), 1),
-                "by_pass": {k: v for k, v in pipe.items() if k != "total"},
+                "by_pass": {k: v for k, v in pipe.items() if k not in ("total", "trace_m", "trace_first")},
                 "image_bytes_per_dispatch": image_bytes,
                 "image_gbs": round(image_bytes / (d_ms * 1e-3) / 1e9, 3)},
         "work": st,
@@ -704,8 +716,11 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
     }
     if shade is not None:
         out["roofline"]["shade"] = shade
-        # the two kernels' fractions of the same peak, each over its own time
-        out["roofline"]["fracs_sum"] = round(out["roofline"]["frac"] + shade["frac"], 4)
+        # the two kernels' executed fractions while they share the GPU (the
+        # timed steps): <= 1 by construction of a consistent accounting; each
+        # one's solo frac (roofline.frac, shade.frac) is over its own time
+        out["roofline"]["overlapped"] = ov
+        out["roofline"]["fracs_sum"] = ov["sum"]
     if eq is not None:
         out["roofline"]["reference_equivalent"] = eq
         out["roofline"]["reference_equivalent_frac"] = eq["trace_frac"]
@@ -723,14 +738,34 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
                       "achieved_gbs": round(d_bytes / (disp_ms * 1e-3) / 1e9, 1), "peak_gbs": PEAK_HBM_GBS,
                       "algorithmic_bytes": d_bytes}
     prof = profiled(out["config"])
-    if prof is not None:
+    if prof is not None and trace_n:
         pd, src = prof
-        hb = pd["derived"]["hbm_bytes_per_launch"]
-        out["roofline"]["traffic"] = hb
-        out["roofline"]["traffic_source"] = f"{src} (2*FETCH_SIZE+WRITE_SIZE, KiB->B, per launch)"
-        out["hbm"]["trace_kernel_measured_bytes_per_launch"] = hb
-        out["roofline"]["hw"] = dict(hw_view(pd["derived"]), source=src)
-        sk = (pd.get("other_kernels") or {}).get(shade["kernel"]) if shade else None
+        pk = pd["per_kernel"]
+        # measured HBM bytes per launch (FETCH_SIZE + WRITE_SIZE, calibrated
+        # on the pipeline's own access shapes: scripts/summarize_profile.py)
+        # next to the same kernel's algorithmic bytes per launch
+        lanes = int(pt.get_option("bin_lanes"))
+        n_first = float(lanes)  # one first pass (pt_bin_trace_g_jit) per pipeline per step
+        n_march = max(1.0, float(np.mean(trace_n)) - n_first)
+        tk = pk.get(hot) or {}
+        if "hbm_bytes_per_launch" in tk:
+            out["roofline"]["traffic"] = tk["hbm_bytes_per_launch"]
+            out["roofline"]["traffic_source"] = (f"{src}: FETCH_SIZE + WRITE_SIZE (KiB -> B) per {hot} launch, one "
+                                                 "pipeline; profiles/r04q_calib_traffic.json: exact for its 64 B "
+                                                 "record gathers and stores")
+            out["roofline"]["traffic_algorithmic"] = round(pipe["trace_m"] / n_march)
+        first = pk.get("pt_bin_trace_g_jit") or {}
+        if gen_trace and "hbm_bytes_per_launch" in first:
+            out["roofline"]["traffic_first_pass"] = {"kernel": "pt_bin_trace_g_jit",
+                                                     "measured": first["hbm_bytes_per_launch"],
+                                                     "algorithmic": round(pipe["trace_first"] / n_first)}
+        sk = pk.get(shade["kernel"]) if shade else None
+        if sk and "hbm_bytes_per_launch" in sk:
+            out["roofline"]["shade"]["traffic"] = sk["hbm_bytes_per_launch"]
+            out["roofline"]["shade"]["traffic_algorithmic"] = round(pipe["shade"] / max(1.0, float(np.mean(shade_n))))
+        out["hbm"]["trace_kernel_measured_bytes_per_launch"] = out["roofline"].get("traffic")
+        if tk:
+            out["roofline"]["hw"] = dict(hw_view(tk), source=src)
         if sk:
             out["roofline"]["shade"]["hw"] = dict(hw_view(sk), source=src)
     if not args.no_cpu_baseline and world == 1:

@@ -47,7 +47,7 @@ SYMBOLS = (
     "pt_dispatch_stats", "pt_set_option", "pt_get_option", "pt_jit_log", "pt_jit_compile", "pt_last_error",
     "pt_destroy", "pt_abi_version", "pt_device_math", "pt_check_sqrt_exhaustive", "pt_check_div_exhaustive",
     "pt_check_div_random", "pt_check_box_random", "pt_check_div_k", "pt_display", "pt_write_accum",
-    "pt_compile_scene_keyed", "pt_save_rgba8", "pt_comm_size",
+    "pt_compile_scene_keyed", "pt_save_rgba8", "pt_comm_size", "pt_traffic_probe",
 )
 PT_MATH = {"max": 0, "min": 1, "sqrt": 2, "sqrtf": 3, "sin": 4, "cos": 5, "div": 6, "fma": 7}
 
@@ -159,6 +159,7 @@ def lib() -> ctypes.CDLL:
         "pt_check_div_random": (c_int, [c_int, c_uint32, c_uint32, POINTER(c_uint64), POINTER(c_uint64)]),
         "pt_check_box_random": (c_int, [c_int, c_uint32, c_uint32, c_int, POINTER(c_uint64)]),
         "pt_check_div_k": (c_int, [c_int, c_float, c_uint32, c_uint32, POINTER(c_uint64), POINTER(c_uint64)]),
+        "pt_traffic_probe": (c_int, [c_int, c_uint32, POINTER(c_float), POINTER(c_uint64)]),
         "pt_display": (c_int, [c_void_p, c_int, c_void_p, c_size_t]),
         "pt_write_accum": (c_int, [c_void_p, POINTER(c_float), c_size_t]),
     }

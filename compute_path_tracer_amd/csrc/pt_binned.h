@@ -48,17 +48,23 @@
 #define PT_SCATTER_ITEMS 16
 #endif
 
-// A path between two segments (ray) or at the hit of its segment (hit
-// record), 64 B = four 16 B quads:
+// A path between two segments (ray) or, taps in the trace pass, at the hit
+// of its segment (hit record), 64 B = four 16 B quads:
 //   q0 = (ro.x, ro.y, ro.z, rd.x)        ro: origin, or the hit point
 //   q1 = (rd.y, rd.z, thr.x, thr.y)
 //   q2 = (thr.z, rng, sid, aux)          sid: sample slot = frame * n_pix + local
-//                                        pixel; aux: the hit's material index, or
-//                                        PT_AUX_MISS (a miss writes only this quad)
+//                                        pixel; aux: a ray's own slot (its index
+//                                        in its buffer), a hit record's material
+//                                        index, or PT_AUX_MISS (a miss writes
+//                                        only this quad)
 //   q3 = ray: check[] bits 0..63 of the segment to trace (64..127: PtPass.mask_hi)
-//        hit, taps in the shade pass: (check[] bits 0..63, the taps' map()
-//        bound, 0) (bits 64..127 in PtPass.hitn.zw)
-//        hit, taps in the trace pass: (calc_normal's differences, 0)
+//        hit record: (calc_normal's differences, 0)
+// With the taps in the shade pass (the scene kernels) the trace pass writes
+// no record: a hit or a miss is one 16 B hit quad (PtPass.hq) at its binned
+// position, {t, material or PT_AUX_MISS, the taps' map() bound, the ray's
+// slot}, and the shade pass reads the traced ray itself from its slot -- the
+// trace pass does not change it -- and recomputes the hit point ro + rd * t
+// with calc_point's f32 steps.  (check[] bits 64..127 of a hit: PtPass.hitn.zw.)
 // The path's radiance (path_trace's `ret`) is not carried: it lives in the
 // sample's colour slot (zeroed by gen), which the shade pass updates when an
 // emission is added and which is final when the path ends.
@@ -68,8 +74,10 @@ struct PtRay {
 
 struct PtPass {
     PtLaunch L;             // scene tables, image, frame0 / last_clear0 of this chunk
-    PtRay *rin;             // this pass's rays, by slot (gen / bounds: the rays being binned)
-    PtRay *rout;            // trace: next pass's rays, by binned position
+    PtRay *rin;             // this pass's rays, by slot (gen: the rays being binned; shade: the traced rays)
+    PtRay *rout;            // trace with taps: its hit records; shade: the next pass's rays (both by binned
+                            // position)
+    uint4 *hq;              // trace -> shade (taps in the shade pass): a hit quad per binned position
     uint2 *mask_hi;         // check[] bits 64..127 per rin slot (scenes with > 64 entries)
     uint32_t *key;          // bin per rin slot (PT_BIN_NONE: no live ray)
     uint32_t *idx;          // rin slots in bin order
@@ -229,7 +237,7 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
         camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), L.width, L.height, L.aspect, L.fov, rng, ro, rd);
         st.add(PT_ST_SAMPLES);
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
-        store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, rng, i, 0u, make_uint4(m.x, m.y, 0u, 0u));
+        store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, rng, i, i, make_uint4(m.x, m.y, 0u, 0u));
         P.color[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the path's radiance (ret) starts at 0
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         if (!P.gen_order) {
@@ -251,11 +259,13 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
 // pass had idle.
 //
 // TAPS = false (PtPass taps_in_shade, scene kernels only): the trace pass
-// stopped at the hit, and this pass evaluates calc_normal's six taps itself
-// (test_compute.glsl:57-66) with Map = JitMapB: all lanes of a wave tap
-// together, and the per-hit map() bound (pt_path.h tap_bound, from the hit
-// record) lets each tap drop every shape that provably lies farther away
-// (DESIGN.md 3.13).
+// stopped at the hit and wrote its hit quad; this pass reads the traced ray
+// from the quad's slot, recomputes the hit point, and evaluates
+// calc_normal's six taps itself (test_compute.glsl:57-66) with Map = JitMapB:
+// all lanes of a wave tap together, and the per-hit map() bound (pt_path.h
+// tap_bound, carried in the quad) lets each tap drop every shape that
+// provably lies farther away.  TAPS = true: the hit records
+// of P.rout, shaded and replaced in place by the next rays.
 template <class Map, bool ST, bool TAPS>
 __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     __shared__ uint32_t lh[PT_BINS];
@@ -278,24 +288,30 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     stt.init();
     const PtLaunch &L = P.L;
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
+    // q0..q3: the traced ray (TAPS = false; hq its hit quad) or the hit
+    // record (TAPS = true)
     auto shade_one = [&](uint32_t i, const uint4 &q0, const uint4 &q1, const uint4 &q2, const uint4 &q3,
-                         const uint2 &hi) {
+                         const uint2 &hi, const uint4 &hq) {
         pt_f3 ro{__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
         pt_f3 rd{__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
         pt_f3 thr{__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
         pt_f3 ret{0.0f, 0.0f, 0.0f};  // this segment's emission (added to the colour slot below)
         uint32_t rng = q2.y;
         const uint32_t sid = q2.z;
-        const int mat = int(q2.w);
+        const int mat = int(TAPS ? q2.w : hq.y);
         int seg = P.bounce;
         // taps in the trace pass: q3 = calc_normal's differences
         float dv0 = __uint_as_float(q3.x), dv1 = __uint_as_float(q3.y), dv2 = __uint_as_float(q3.z);
         if constexpr (!TAPS) {
+            // the hit point: calc_point's f32 steps with the trace's t
+            // (pt_path.h after_map), so the same bits
+            const float t = __uint_as_float(hq.x);
+            ro = pt_f3{ro.x + rd.x * t, ro.y + rd.y * t, ro.z + rd.z * t};
             // (the taps' counters go to their own half of the stats buffer:
             // pt_dispatch_stats sums both, bench.py splits the flops by pass)
-            // hit record: q3 = {check[] bits 0..63, tap bound}, hi = check[] bits 64..127
+            // the ray's check[] bits 0..63 (q3.xy) and 64..127 (hi)
             Check ck{uint64_t(q3.x) | (uint64_t(q3.y) << 32), uint64_t(hi.x) | (uint64_t(hi.y) << 32)};
-            const float bnd = __uint_as_float(q3.z);
+            const float bnd = __uint_as_float(hq.z);
             // bnd widened by the taps' spread (two taps are at most 2e apart,
             // plus their coordinates' rounding): the first tap's tests against
             // it leave in `live` every shape any tap may need
@@ -345,24 +361,35 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             return;
         }
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
-        store_ray(P.rin + i, ro, rd, thr, rng, sid, 0u, make_uint4(m.x, m.y, 0u, 0u));
+        store_ray(P.rout + i, ro, rd, thr, rng, sid, i, make_uint4(m.x, m.y, 0u, 0u));
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_of(m);
         P.key[i] = k;
         atomicAdd(&lh[k], 1u);
     };
-    // Nearly every position holds a hit (misses end in the trace pass), so
-    // each thread takes one position and loads its whole record (a miss
-    // marks its record's q2): one memory round trip.
+    // One thread per binned position.  TAPS = false: its hit quad, then the
+    // traced ray from the quad's slot; TAPS = true: its hit record (a miss
+    // marks its record's q2).
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint4 q0 = P.rin[i].q[0], q1 = P.rin[i].q[1], q2 = P.rin[i].q[2], q3 = P.rin[i].q[3];
-        uint2 hi = make_uint2(0u, 0u);
-        if (!TAPS && wide_of<Map>(P)) {
-            const float4 nd = P.hitn[i];
-            hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
+        if constexpr (TAPS) {
+            const uint4 q0 = P.rout[i].q[0], q1 = P.rout[i].q[1], q2 = P.rout[i].q[2], q3 = P.rout[i].q[3];
+            if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
+            else shade_one(i, q0, q1, q2, q3, make_uint2(0u, 0u), q3);
+        } else {
+            const uint4 hq = P.hq[i];
+            if (hq.y == PT_AUX_MISS) {
+                P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
+                continue;
+            }
+            const PtRay *r = P.rin + hq.w;
+            const uint4 q0 = r->q[0], q1 = r->q[1], q2 = r->q[2], q3 = r->q[3];
+            uint2 hi = make_uint2(0u, 0u);
+            if (wide_of<Map>(P)) {
+                const float4 nd = P.hitn[i];
+                hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
+            }
+            shade_one(i, q0, q1, q2, q3, hi, hq);
         }
-        if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
-        else shade_one(i, q0, q1, q2, q3, hi);
     }
     hist_flush(lh, P.hist);
     flush_stats<ST>(L, st);
@@ -465,13 +492,15 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
 // a shaded path either ends (colour stored, end marker written) or writes
 // its next ray to rout at its binned position.
 //
-// TAPS = false: a lane stops at the hit (calc_point) and writes the hit
-// record for the shade pass, which evaluates the normal taps (bin_shade_body).
+// TAPS = false: a lane stops at the hit and writes its 16 B hit quad for the
+// shade pass (PtPass.hq), which reads the ray itself from its slot and
+// evaluates the normal taps (bin_shade_body).
 //
 // GEN (PtPass gen_trace, the first pass in generation order): a window's
 // rays are not loaded but made here, lane j the camera ray and bounds() mask
 // of sample wbase + j -- what gen would have written (bin_gen_body), with
-// all 64 lanes at once -- so the chunk needs no gen pass.
+// all 64 lanes at once, stored to its slot for the shade pass -- so the
+// chunk needs no gen pass.
 template <class Map, bool ST, bool TAPS = true, bool GEN = false>
 __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     // the staged window, once its loads have landed: [part][lane], so a
@@ -559,7 +588,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             const uint4 m = MapBounds<Map>::template mask<ST>(L, o, d, st);
             s0 = make_float4(o.x, o.y, o.z, d.x);
             s1 = make_float4(d.y, d.z, 1.0f, 1.0f);
-            s2 = make_float4(1.0f, __uint_as_float(rg), __uint_as_float(i), 0.0f);
+            s2 = make_float4(1.0f, __uint_as_float(rg), __uint_as_float(i), __uint_as_float(i));  // (aux: its slot)
             s3 = make_uint4(m.x, m.y, 0u, 0u);
             sh = make_uint2(m.z, m.w);
         } else if (uint32_t(lane) < wcnt) {
@@ -580,7 +609,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     stage();
 
     int state = ST_FREE;
-    uint32_t rng = 0u, sid = 0u, pos = 0u;
+    uint32_t rng = 0u, sid = 0u, pos = 0u, slot = 0u;
     pt_f3 ro{0.0f, 0.0f, 0.0f}, rd{0.0f, 0.0f, 1.0f};
     pt_f3 thr{1.0f, 1.0f, 1.0f};
     int step = 0, mat = 0;  // (a lane's segment index is this pass's P.bounce)
@@ -595,15 +624,15 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                     const pt_f3 c = final_color(L.debug, P.bounce, L.bounces, pt_f3{0.0f, 0.0f, 0.0f});
                     P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
                 }
-                P.rout[pos].q[2] = make_uint4(0u, 0u, sid, PT_AUX_MISS);
+                if constexpr (TAPS) P.rout[pos].q[2] = make_uint4(0u, 0u, sid, PT_AUX_MISS);
+                else P.hq[pos] = make_uint4(0u, PT_AUX_MISS, 0u, slot);
                 if constexpr (GEN) P.color[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // (no gen pass zeroed it)
             } else {
-                if constexpr (TAPS) {  // normal differences
+                if constexpr (TAPS) {  // hit record: hit point + normal differences
                     store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
                               make_uint4(__float_as_uint(dv0), __float_as_uint(dv1), __float_as_uint(dv2), 0u));
-                } else {  // hit point + check[] + tap bound + material (bin_shade_body)
-                    store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
-                              make_uint4(uint32_t(ck.lo), uint32_t(ck.lo >> 32), __float_as_uint(dv0), 0u));
+                } else {  // hit quad: t, material, tap bound, slot (bin_shade_body)
+                    P.hq[pos] = make_uint4(__float_as_uint(t), uint32_t(mat), __float_as_uint(dv0), slot);
                     if (wide_of<Map>(P))
                         P.hitn[pos] = make_float4(0.0f, 0.0f, __uint_as_float(uint32_t(ck.hi)),
                                                   __uint_as_float(uint32_t(ck.hi >> 32)));
@@ -634,6 +663,21 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         W[3][lane] = s3;
         if constexpr (MapWide<Map>::v != 0)
             if (wide_of<Map>(P)) W[4][lane] = make_uint4(sh.x, sh.y, 0u, 0u);
+        if constexpr (GEN) {
+            // the window's camera rays at their slots for the shade pass: 64
+            // lanes, 64 contiguous records (whole lines)
+            if (in_win) {
+                uint4 *r = reinterpret_cast<uint4 *>(P.rin + wbase + uint32_t(lane));
+                r[0] = make_uint4(__float_as_uint(s0.x), __float_as_uint(s0.y), __float_as_uint(s0.z),
+                                  __float_as_uint(s0.w));
+                r[1] = make_uint4(__float_as_uint(s1.x), __float_as_uint(s1.y), __float_as_uint(s1.z),
+                                  __float_as_uint(s1.w));
+                r[2] = make_uint4(__float_as_uint(s2.x), __float_as_uint(s2.y), __float_as_uint(s2.z),
+                                  __float_as_uint(s2.w));
+                r[3] = s3;
+                if (wide_of<Map>(P)) P.mask_hi[wbase + uint32_t(lane)] = sh;
+            }
+        }
         in_lds = true;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -678,7 +722,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 thr = pt_f3{b2, b3, c0};
                 rng = __float_as_uint(c1);
                 sid = __float_as_uint(c2);
-                (void)c3;
+                slot = __float_as_uint(c3);  // (a ray's aux: its slot)
                 ck.lo = uint64_t(d0) | (uint64_t(d1) << 32);
                 (void)d2;
                 (void)d3;

@@ -95,7 +95,8 @@ struct pt_ctx {
     // another's VALU-bound trace pass and fill its tail.  bin_cap samples per
     // lane; the colour buffer holds the whole chunk.
     struct BinLane {
-        PtRay *ray[2] = {nullptr, nullptr};  // ping-pong: pass k reads ray[k & 1], writes the other
+        PtRay *ray[2] = {nullptr, nullptr};  // ping-pong: pass k traces ray[k & 1], its shade pass writes the other
+        uint4 *hq = nullptr;                 // trace -> shade: the hit quads (taps in the shade pass)
         uint2 *mask_hi = nullptr;            // check[] bits 64..127 (scenes with > 64 entries)
         uint32_t *key = nullptr, *idx = nullptr, *hist = nullptr, *offs = nullptr, *ctrl = nullptr;
         float4 *hitn = nullptr;  // trace -> shade: normal differences per position
@@ -620,9 +621,10 @@ int pt_set_tiles(pt_ctx *c, uint32_t rank, uint32_t nranks) {
 }
 
 // ---- binned pipeline (pt_binned.h) -------------------------------------------
-// per sample of a chunk: two ray buffers, bin key, binned slot, colour (+ the
-// high mask words and hit records' high check[] words of scenes with > 64 entries)
-constexpr size_t kBinBytesPerSample = 2 * sizeof(PtRay) + 2 * sizeof(uint32_t) + sizeof(float4);
+// per sample of a chunk: two ray buffers, hit quad, bin key, binned slot,
+// colour (+ the high mask words and hits' high check[] words of scenes with
+// > 64 entries)
+constexpr size_t kBinBytesPerSample = 2 * sizeof(PtRay) + sizeof(uint4) + 2 * sizeof(uint32_t) + sizeof(float4);
 constexpr size_t kBinBytesWide = sizeof(uint2) + sizeof(float4);
 
 static size_t bin_bytes_per_sample(const pt_ctx *c) {
@@ -630,7 +632,7 @@ static size_t bin_bytes_per_sample(const pt_ctx *c) {
 }
 
 // Samples per chunk: pt_set_option "bin_samples", else automatic: 2^29 (a
-// whole 256-spp 1080p render: 82 GB of HBM at 152 B per sample; every pass's
+// whole 256-spp 1080p render: 90 GB of HBM at 168 B per sample; every pass's
 // tail is paid once per chunk, so larger chunks are faster: 64 -> 256 frames
 // per chunk +5 %), at most half of what this context could hold on its
 // device -- the free memory plus the chunk buffers it already owns (other
@@ -659,6 +661,7 @@ static void free_bin(pt_ctx *c) {
     for (auto &l : c->lane) {
         (void)hipFree(l.ray[0]);
         (void)hipFree(l.ray[1]);
+        (void)hipFree(l.hq);
         (void)hipFree(l.mask_hi);
         (void)hipFree(l.key);
         (void)hipFree(l.idx);
@@ -691,6 +694,7 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
         pt_ctx::BinLane &l = c->lane[i];
         ok = hipMalloc(&l.ray[0], samples * sizeof(PtRay)) == hipSuccess &&
              hipMalloc(&l.ray[1], samples * sizeof(PtRay)) == hipSuccess &&
+             hipMalloc(&l.hq, samples * sizeof(uint4)) == hipSuccess &&
              (c->n_check <= 64 || hipMalloc(&l.mask_hi, samples * sizeof(uint2)) == hipSuccess) &&
              hipMalloc(&l.key, samples * sizeof(uint32_t)) == hipSuccess &&
              hipMalloc(&l.idx, samples * sizeof(uint32_t)) == hipSuccess &&
@@ -832,6 +836,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             p.L.spp = int32_t(fl[i]);
             p.rin = l.ray[0];
             p.rout = l.ray[1];
+            p.hq = l.hq;
             p.mask_hi = l.mask_hi;
             p.key = l.key;
             p.idx = l.idx;
@@ -883,12 +888,15 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 HIPCHK(c, hipGetLastError());
             }
         }
-        // shade the hits trace pass k wrote into ray[(k + 1) & 1]: ended paths
-        // store their colour, the rest get their next ray, bounds() and bin
+        // shade the hits of trace pass k (its hit quads and the rays it traced,
+        // ray[k & 1]; or, taps in the trace pass, its hit records in
+        // ray[(k + 1) & 1]): ended paths store their colour, the rest get
+        // their next ray in ray[(k + 1) & 1], bounds() and bin
         auto shade = [&](int i, int k) -> int {
             PtPass S = P[i];
             S.bounce = k;
-            S.rin = c->lane[i].ray[(k + 1) & 1];
+            S.rin = c->lane[i].ray[k & 1];
+            S.rout = c->lane[i].ray[(k + 1) & 1];
             S.n_src = c->lane[i].ctrl + size_t(PT_CTRL_STRIDE) * k;
             if (!stats) HIPCHK(c, record_event(c->slog, c->lane[i].stream));
             if (taps_shade) {

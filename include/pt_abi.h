@@ -230,7 +230,7 @@ int pt_display(pt_ctx *ctx, int format, void *out, size_t bytes);
  * rays of a chunk of frames are grouped by their bounds() check set before
  * they are marched), "shade_batch" (state-machine kernels: lanes that must
  * wait before a shading pass runs, 1..64), "bin_samples" (binned kernel:
- * samples per chunk, >= 64; device memory = 152 B per sample, 176 B for
+ * samples per chunk, >= 64; device memory = 168 B per sample, 192 B for
  * scenes with > 64 check[] entries; default 2^29 samples, at most half of
  * the device memory this context could hold), "bin_lanes"
  * (binned kernel: 1..4 pipelines, each on its own stream, over which a
@@ -297,6 +297,11 @@ int pt_check_box_random(int hip_device, uint32_t seed, uint32_t n, int mode, uin
  * scale constant, |b| in [2^-4, 2^4]) against the IEEE a / b, bit for bit,
  * for the na patterns a0 .. a0 + na - 1 (na a multiple of 256). */
 int pt_check_div_k(int hip_device, float b, uint32_t a0, uint32_t na, uint64_t *mismatches, uint64_t *first_bad);
+/* Calibration probes for rocprofv3's FETCH_SIZE / WRITE_SIZE on the
+ * pipeline's access shapes (pt_probe.hip): 2^log2n items (16..26) of, in
+ * order, a 64 B record gather, a 16 B coalesced read, a 16 B scattered store
+ * and a 64 B record store; ms[k] = device time, bytes[k] = bytes moved. */
+int pt_traffic_probe(int hip_device, uint32_t log2n, float ms[4], uint64_t bytes[4]);
 
 #ifdef __cplusplus
 }

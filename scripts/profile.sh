@@ -4,7 +4,7 @@
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${PROF_TAG:-r01}"
-OUT="$R/gpurun_out/prof_$TAG"
+OUT="${GPU_OUT:-$R/gpurun_out}/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 ARGS="${PROF_ARGS:---steps 4 --warmup 1 --no-cpu-baseline}"
@@ -18,7 +18,7 @@ if [ "${1:-}" = "pmc" ]; then
   for p in "${PASSES[@]}"; do
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $p --kernel-trace -d "$OUT/pmc$i" -o pmc --output-format csv -- \
-        python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc${i}.log" 2>&1
+        python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline ${PMC_ARGS:-} > "$OUT/pmc${i}.log" 2>&1
     rc=$?; echo "pmc pass $i ($p) rc=$rc"
     [ $rc -eq 0 ] || exit $rc
   done

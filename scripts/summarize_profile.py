@@ -6,12 +6,20 @@ profiles/<tag>_pmc.json (per-launch counters of the hot kernel and derived
 metrics, plus the derived metrics of the other pipeline kernels) and
 profiles/<tag>_summary.md.
 
-HBM bytes per launch follow MI355X_MICROARCH.md "HBM": FETCH_SIZE reads
-exactly half of a wide coalesced stream on gfx950 (16 B/lane loads, which is
-what the kernels' float4 ray / texel loads are), so bytes = 2*FETCH_SIZE*1024
-+ WRITE_SIZE*1024 (WRITE_SIZE is exact for 16 B/lane stores); each counter
-from its own pass.  The hot kernel is the binned trace pass when present
-(averages over its launches), else the tile-resident kernel.
+HBM bytes per launch: FETCH_SIZE*1024 + WRITE_SIZE*1024, each counter from
+its own pass.  MI355X_MICROARCH.md ("HBM") has FETCH_SIZE at exactly half of
+a wide coalesced 16 B/lane read and leaves other shapes uncalibrated; the
+pipeline's own shapes were calibrated with known-byte probes (pt_probe.hip,
+profiles/r04q_calib_traffic.json): a 64 B record gathered by slot reads
+FETCH_SIZE = its bytes (ratio 1.0), a 64 B record store WRITE_SIZE = its
+bytes, a 16 B store at a scattered position WRITE_SIZE = 2x (a 32 B write
+granule moved), a 16 B/lane coalesced read FETCH_SIZE = half.  The trace
+and shade passes' traffic is dominated by the exact shapes (64 B gathers and
+stores), so the sum is used as is: what the memory side moved, up to the
+coalesced 16 B reads' undercount (the shade pass's hit quads, the slot list).
+The hot kernel is the binned trace pass when present (averages over its
+launches), else the tile-resident kernel; every kernel's figures are in
+per_kernel.
 """
 from __future__ import annotations
 
@@ -48,7 +56,9 @@ def collect(src: str) -> dict:
 def derive(c: dict) -> dict:
     d = {}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-        d["hbm_bytes_per_launch"] = 2.0 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
+        d["fetch_bytes_per_launch"] = c["FETCH_SIZE"] * 1024
+        d["write_bytes_per_launch"] = c["WRITE_SIZE"] * 1024
+        d["hbm_bytes_per_launch"] = d["fetch_bytes_per_launch"] + d["write_bytes_per_launch"]
     if "SQ_THREAD_CYCLES_VALU" in c and c.get("SQ_ACTIVE_INST_VALU"):
         d["valu_lane_utilization"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
     if c.get("GRBM_GUI_ACTIVE") and c.get("SQ_INSTS_VALU"):
@@ -95,7 +105,16 @@ def main(tag: str, src: str = None) -> None:
     trace_avg = sum(float(r["TotalDurationNs"]) for r in trace_rows) * 1e-9 / calls if calls else None
     if ktime and "hbm_bytes_per_launch" in d:
         d["hbm_gbs_measured"] = d["hbm_bytes_per_launch"] / ktime / 1e9
-    others = {}
+    others, every = {}, {}
+    for n, (c, m) in sorted(per_kernel.items()):
+        if "<true>" in n or "stats" in n:
+            continue
+        ed = derive(c)
+        kt = avg_s(n)
+        ed["avg_s_kernel_trace"] = kt
+        if kt and "hbm_bytes_per_launch" in ed:
+            ed["hbm_gbs_measured"] = ed["hbm_bytes_per_launch"] / kt / 1e9
+        every[n] = dict(ed, vgpr=m.get("vgpr"), grid=m.get("grid"))
     for n, (c, _) in sorted(per_kernel.items()):
         if n == hot or "<true>" in n or "stats" in n:
             continue
@@ -113,7 +132,7 @@ def main(tag: str, src: str = None) -> None:
            "bench_shade_ms_hip_events": (bench_line["roofline"].get("shade") or {}).get("ms_per_launch")
            if bench_line else None,
            "shade_avg_s_kernel_trace": avg_s("pt_bin_shade_t_jit"),
-           "other_kernels": others}
+           "other_kernels": others, "per_kernel": every}
     with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     lines = [f"# rocprofv3 summary `{tag}`", "",

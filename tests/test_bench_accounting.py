@@ -53,7 +53,8 @@ def test_pipeline_bytes_add_up(counters):
     _, ct, pixels = counters
     for gen_trace in (True, False):
         parts = bench.pipeline_bytes(ct, pixels, gen_trace=gen_trace)
-        assert parts["total"] == pytest.approx(sum(v for k, v in parts.items() if k != "total"))
+        assert parts["total"] == pytest.approx(sum(v for k, v in parts.items() if k not in ("total", "trace_m", "trace_first")))
+        assert parts["trace_m"] + parts["trace_first"] == pytest.approx(parts["trace"])
         assert parts["fold"] == 16.0 * ct["samples"] + 32.0 * pixels
 
 
@@ -95,3 +96,19 @@ def test_gpus_mismatch_exits_before_the_gpu():
                        timeout=120)
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr and not any(l.startswith("{") for l in r.stdout.splitlines())
+
+
+def test_executed_flops_drop_only_culled_work(counters):
+    """roofline.frac's executed flops: each pass's algorithmic flops less its
+    culled evaluations, each culled one still paying its test; without culls
+    the two agree."""
+    prog, ct, _ = counters
+    st = dict(ct, wave_maps=0, wave_shapes=0)
+    taps = _taps_share(ct)
+    alg = (bench.trace_flops(st, taps, prog.n_aabb, True), bench.shade_flops(st, taps, prog.n_aabb))
+    assert bench.executed_split(dict(st, culled=0), taps, prog.n_aabb, True) == pytest.approx(alg)
+    st_c = dict(st, culled=st["xform_shape"] // 2)
+    ex = bench.executed_split(st_c, taps, prog.n_aabb, True)
+    assert ex[0] < alg[0] and ex[1] == pytest.approx(alg[1])
+    per = bench.W_XFORM + bench.W_FINALISE + 1 - bench.W_CULL_TEST
+    assert alg[0] - ex[0] >= st_c["culled"] * per  # (plus the mean SDF weight)
