@@ -214,6 +214,11 @@ def hw_view(derived: dict) -> dict:
     out = {k: round(derived[k], 4) for k in keys if k in derived}
     if "valu_issue_frac_of_peak" in out and "valu_lane_utilization" in out:
         out["valu_lane_slots_busy"] = round(derived["valu_issue_frac_of_peak"] * derived["valu_lane_utilization"], 4)
+    if derived.get("fp32_tflops_measured"):
+        # the FP32 flops the kernel executed by its own instruction counts
+        # (add/mul 1, fma 2, at its lane utilisation) over its time
+        out["fp32_tflops_measured"] = round(derived["fp32_tflops_measured"], 3)
+        out["fp32_frac_measured"] = round(derived["fp32_tflops_measured"] / PEAK_F32_TFLOPS, 4)
     return out
 
 

@@ -67,6 +67,16 @@ def derive(c: dict) -> dict:
         d["valu_issue_per_simd_cycle"] = c["SQ_INSTS_VALU"] / (1024.0 * cyc)
         d["valu_issue_frac_of_peak"] = d["valu_issue_per_simd_cycle"] / 0.5  # wave64 VALU = 2 cycles on SIMD32
         d["salu_per_valu"] = c.get("SQ_INSTS_SALU", 0.0) / c["SQ_INSTS_VALU"]
+    if "SQ_INSTS_VALU_FMA_F32" in c and "valu_lane_utilization" in d:
+        # FP32 flops the kernel executed, from its instruction counts: add and
+        # mul 1, fma 2 per lane (transcendentals excluded, as in the
+        # algorithmic weights), at the kernel's mean VALU lane utilisation
+        ops = c.get("SQ_INSTS_VALU_ADD_F32", 0.0) + c.get("SQ_INSTS_VALU_MUL_F32", 0.0) + \
+            2.0 * c["SQ_INSTS_VALU_FMA_F32"]
+        d["fp32_flops_per_launch"] = ops * 64.0 * d["valu_lane_utilization"]
+        d["fp32_trans_insts_per_launch"] = c.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
+        if c.get("SQ_INSTS_VALU"):
+            d["fp32_insts_frac_of_valu"] = (ops - c["SQ_INSTS_VALU_FMA_F32"]) / c["SQ_INSTS_VALU"]
     if c.get("SQ_WAVE_CYCLES"):
         tot = c["SQ_WAVE_CYCLES"]
         d["wave_time_active"] = c.get("SQ_ACTIVE_INST_ANY", 0.0) / tot
@@ -114,6 +124,8 @@ def main(tag: str, src: str = None) -> None:
         ed["avg_s_kernel_trace"] = kt
         if kt and "hbm_bytes_per_launch" in ed:
             ed["hbm_gbs_measured"] = ed["hbm_bytes_per_launch"] / kt / 1e9
+        if kt and "fp32_flops_per_launch" in ed:
+            ed["fp32_tflops_measured"] = ed["fp32_flops_per_launch"] / kt / 1e12
         every[n] = dict(ed, vgpr=m.get("vgpr"), grid=m.get("grid"))
     for n, (c, _) in sorted(per_kernel.items()):
         if n == hot or "<true>" in n or "stats" in n:
