@@ -280,24 +280,36 @@ def cpu_baseline(scene, w, h, bounces, threads: int, row_stride: int, spp, targe
     samples = rows * w * spp
     quota = info["quota"]
     return {"value": samples / dt / 1e6, "unit": "Msamples/sec", "cores": threads, "kind": "port",
-            "cpu_model": info["model"], "os_cpu_count": info["os_cpu_count"], "cpus_available": info["affinity"],
-            "cgroup_cpu_quota": quota,
-            "sample": f"C oracle ({build}, pthreads: {threads} threads = every CPU in this process's affinity "
-                      f"mask{'' if quota is None else f'; the cgroup allows {quota} CPUs of time'}) on every "
+            "cpu_model": info["model"], "os_cpu_count": info["os_cpu_count"], "cpus_available": usable_cpus(info),
+            "cpu_affinity": info["affinity"], "cgroup_cpu_quota": quota,
+            "sample": f"C oracle ({build}, pthreads: {threads} threads; this process may use {usable_cpus(info)} "
+                      f"CPUs at once: affinity mask {info['affinity']}"
+                      f"{'' if quota is None else f', cgroup quota {quota} CPUs of time'}) on every "
                       f"{row_stride}th row of the same {w}x{h} {bounces}-bounce frame, {spp} spp ({samples} "
                       f"samples, {dt:.1f} s; spp set by a {cal:.1f} s 1-spp calibration run)"}
 
 
+def usable_cpus(info: dict) -> int:
+    """The CPUs this process can actually run on at once: its affinity mask,
+    capped by the cgroup's CPU quota (cpu.max) where one is set -- more
+    threads than the quota only time-share it (measured on the GPU box: 256
+    threads under a 16-CPU quota ran 0.47 Msamples/s, 16 threads ~0.78)."""
+    n = info["affinity"]
+    if info.get("quota"):
+        n = min(n, max(1, int(info["quota"])))
+    return max(1, n)
+
+
 def default_cpu_threads() -> int:
-    """Every CPU this process may use (its affinity mask): the oracle runs
-    pthreads, so OMP_NUM_THREADS does not apply."""
-    return max(1, cpu_info()["affinity"])
+    """One pthread per usable CPU (usable_cpus): the oracle runs pthreads,
+    so OMP_NUM_THREADS does not apply."""
+    return usable_cpus(cpu_info())
 
 
 def solo_pipeline(pt, aspect: float, frames_step: int) -> dict:
     """Per-kernel times for the roofline (outside the timed region): one
-    dispatch of ONE pipeline's share of a step (ceil(frames / pipelines)
-    frames, so the chunk buffers fit as they are) with bin_lanes 1.  Its trace
+    dispatch of ONE pipeline's share of a chunk (ceil(frames per chunk /
+    pipelines) frames, so the chunk buffers fit as they are) with bin_lanes 1.  Its trace
     and shade passes then run alone, so each launch's HIP-event time is the
     kernel's own -- in the timed steps the two pipelines' kernels share the
     GPU and their event times overlap.  The instrumented twin of the same
@@ -305,7 +317,10 @@ def solo_pipeline(pt, aspect: float, frames_step: int) -> dict:
     from compute_path_tracer_amd import _native as N
 
     lanes = int(pt.get_option("bin_lanes"))
-    frames = -(-frames_step // lanes)
+    w, h = pt.size
+    n_pix = -(-w // 8) * -(-h // 8) * 64  # (one rank: every 8x8 tile)
+    chunk = max(1, min(frames_step, int(pt.get_option("bin_samples")) // n_pix))  # frames per chunk
+    frames = -(-chunk // lanes)  # one pipeline's share of a chunk: the buffers fit as they are
     c = N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1)
     pt.set_option("bin_lanes", 1)
     try:
@@ -697,6 +712,7 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
                      "kernel_scope": "trace passes (the first with its camera rays and primary bounds()): march "
                                      "map() work + 10 per step" if gen_trace else "trace passes: march",
                      "kernel_ms_per_launch": round(k_ms, 3), "kernel_launches_per_step": launches,
+                     "solo_launches": solo["trace_n"] if solo is not None else None,
                      "dispatch_ms_per_step": round(d_ms, 3),
                      "path_achieved": round(path_tf, 3), "path_frac": round(path_tf / PEAK_F32_TFLOPS, 4)},
         "hbm": {"achieved": round(achieved_gbs, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -752,21 +768,25 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
         lanes = int(pt.get_option("bin_lanes"))
         n_first = float(lanes)  # one first pass (pt_bin_trace_g_jit) per pipeline per step
         n_march = max(1.0, float(np.mean(trace_n)) - n_first)
+        # the profile ran one pipeline: a launch there carries `lanes` times
+        # the frames of a launch here
+        scale = float(pd["bench_config"].get("pipelines", 1)) / float(lanes)
         tk = pk.get(hot) or {}
         if "hbm_bytes_per_launch" in tk:
-            out["roofline"]["traffic"] = tk["hbm_bytes_per_launch"]
-            out["roofline"]["traffic_source"] = (f"{src}: FETCH_SIZE + WRITE_SIZE (KiB -> B) per {hot} launch, one "
-                                                 "pipeline; profiles/r04q_calib_traffic.json: exact for its 64 B "
-                                                 "record gathers and stores")
+            out["roofline"]["traffic"] = round(tk["hbm_bytes_per_launch"] * scale)
+            out["roofline"]["traffic_source"] = (f"{src} (one pipeline, scaled to this run's launch size): "
+                                                 f"FETCH_SIZE + WRITE_SIZE (KiB -> B) per {hot} launch; "
+                                                 "profiles/r04q_calib_traffic.json: the counters are exact for its "
+                                                 "64 B record gathers and stores")
             out["roofline"]["traffic_algorithmic"] = round(pipe["trace_m"] / n_march)
         first = pk.get("pt_bin_trace_g_jit") or {}
         if gen_trace and "hbm_bytes_per_launch" in first:
             out["roofline"]["traffic_first_pass"] = {"kernel": "pt_bin_trace_g_jit",
-                                                     "measured": first["hbm_bytes_per_launch"],
+                                                     "measured": round(first["hbm_bytes_per_launch"] * scale),
                                                      "algorithmic": round(pipe["trace_first"] / n_first)}
         sk = pk.get(shade["kernel"]) if shade else None
         if sk and "hbm_bytes_per_launch" in sk:
-            out["roofline"]["shade"]["traffic"] = sk["hbm_bytes_per_launch"]
+            out["roofline"]["shade"]["traffic"] = round(sk["hbm_bytes_per_launch"] * scale)
             out["roofline"]["shade"]["traffic_algorithmic"] = round(pipe["shade"] / max(1.0, float(np.mean(shade_n))))
         out["hbm"]["trace_kernel_measured_bytes_per_launch"] = out["roofline"].get("traffic")
         if tk:

@@ -85,6 +85,24 @@ def derive(c: dict) -> dict:
     return d
 
 
+def launch_split(src: str, n_solo: int) -> dict:
+    """Average kernel-trace durations (ms) of the trace passes (march-only +
+    first pass) and the shade passes, split into bench.py's last n_solo
+    launches of each (its one-pipeline solo dispatch, the roofline's timing)
+    and all earlier ones (warm-up and timed steps)."""
+    f = os.path.join(src, "kt", "kt_kernel_trace.csv")
+    if not os.path.exists(f) or n_solo <= 0:
+        return {}
+    rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+    out = {}
+    for key, names in (("trace", ("pt_bin_trace_m_jit", "pt_bin_trace_g_jit")), ("shade", ("pt_bin_shade_t_jit",))):
+        ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in rows if r["Kernel_Name"] in names]
+        if len(ms) > n_solo:
+            out[key + "_solo_ms"] = sum(ms[-n_solo:]) / n_solo
+            out[key + "_timed_ms"] = sum(ms[:-n_solo]) / (len(ms) - n_solo)
+    return out
+
+
 def main(tag: str, src: str = None) -> None:
     src = src or os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
@@ -145,6 +163,19 @@ def main(tag: str, src: str = None) -> None:
            if bench_line else None,
            "shade_avg_s_kernel_trace": avg_s("pt_bin_shade_t_jit"),
            "other_kernels": others, "per_kernel": every}
+    # bench.py's own HIP-event times next to the kernel trace of the same run:
+    # its solo dispatch (the roofline's timing) and the steps before it
+    rl = bench_line["roofline"] if bench_line else {}
+    n_solo = rl.get("solo_launches") or ((rl.get("shade") or {}).get("launches")
+                                         if str(rl.get("timing", "")).startswith("one pipeline alone") else None)
+    if n_solo:
+        ls = launch_split(src, int(n_solo))
+        eq = bench_line["roofline"].get("reference_equivalent") or {}
+        out["event_vs_trace_ms"] = {
+            "trace_solo": (bench_line["roofline"]["kernel_ms_per_launch"], ls.get("trace_solo_ms")),
+            "shade_solo": ((bench_line["roofline"].get("shade") or {}).get("ms_per_launch"), ls.get("shade_solo_ms")),
+            "trace_steps": (eq.get("trace_ms_per_launch"), ls.get("trace_timed_ms")),
+            "shade_steps": (eq.get("shade_ms_per_launch"), ls.get("shade_timed_ms"))}
     with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     lines = [f"# rocprofv3 summary `{tag}`", "",
@@ -153,6 +184,10 @@ def main(tag: str, src: str = None) -> None:
              "## Kernel stats", "", "| kernel | calls | avg ms | % |", "|---|---|---|---|"]
     for r in stats:
         lines.append(f"| {r['Name']} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | {float(r['Percentage']):.2f} |")
+    if out.get("event_vs_trace_ms"):
+        lines += ["", "bench.py HIP events vs rocprofv3 kernel trace, ms per launch (trace = march-only + first pass):"]
+        for k, (ev, kt) in out["event_vs_trace_ms"].items():
+            lines.append(f"- {k}: events {ev}, kernel trace {kt}")
     lines += ["", f"HIP-event time per trace launch inside bench.py: "
                   f"{out['bench_kernel_ms_hip_events']} ms; rocprofv3 over the same launches "
                   f"({hot} + pt_bin_trace_g_jit, launch-weighted): "

@@ -64,7 +64,9 @@ def test_hw_view_and_cpu_info():
     info = bench.cpu_info()
     assert info["os_cpu_count"] >= 1 and info["affinity"] >= 1 and info["model"]
     assert 1 <= bench.default_cpu_threads() <= info["affinity"]
-    assert bench.default_cpu_threads() == info["affinity"]  # every CPU: the oracle is pthreads, not OpenMP
+    assert bench.default_cpu_threads() == bench.usable_cpus(info)  # every usable CPU: pthreads, not OpenMP
+    assert bench.usable_cpus(dict(info, affinity=256, quota=16.0)) == 16
+    assert bench.usable_cpus(dict(info, affinity=8, quota=None)) == 8
 
 
 def test_resolve_world():
