@@ -335,14 +335,155 @@ def solo_pipeline(pt, aspect: float, frames_step: int) -> dict:
         pt.set_option("bin_lanes", lanes)
 
 
-def max_over_ranks(dist, v: float, device: str) -> float:
+def table_kernel_leg(pt, prog, aspect: float, frames: int, steps: int = 2) -> dict:
+    """Throughput of the table scene kernel (outside the timed region).  The
+    headline runs the values-baked build (jit_bake 2's tier-up, installed in
+    setup by jit_wait).  A value edit (DataArray::update, primitives.rs:
+    131-151: a buffer refresh, no recompile) drops that build, and an editing
+    session renders on the table kernel -- node values read from the table --
+    until the rebuild for the new values lands.  This times that kernel on
+    the same workload: jit_bake 0 + the same values, one warm-up and `steps`
+    dispatches of `frames` frames, wall time around each; then the baked
+    build is restored."""
+    from compute_path_tracer_amd import _native as N
+
+    w, h = pt.size
+    c = N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1)
+    pt.set_option("jit_bake", 0)
+    pt.set_data(prog.data)
+    try:
+        if pt.get_option("jit_tier_active") or not pt.get_option("jit_active"):
+            return None  # (not the table kernel: nothing to report)
+        pt.dispatch(c, frames)
+        pt.sync()
+        ts = []
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            pt.dispatch(c, frames)
+            pt.sync()
+            ts.append(time.perf_counter() - t0)
+        dt = float(np.mean(ts))
+        return {"value": round(w * h * frames / dt / 1e6, 3), "unit": "Msamples/sec",
+                "ms_per_step": round(dt * 1e3, 3), "steps": steps,
+                "kernel": "table scene kernel (jit_bake 0: node values read from the table; what renders between "
+                          "a value edit and its values-baked rebuild)"}
+    finally:
+        pt.set_option("jit_bake", 2)
+        pt.set_data(prog.data)
+        pt.set_option("jit_wait", 1)
+
+
+def max_over_ranks(dist, v: float, device: str, op: str = "MAX") -> float:
     if dist is None:
         return v
     import torch
 
     t = torch.tensor([v], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=getattr(dist.ReduceOp, op))
     return float(t.item())
+
+
+def check_tiles_spec(n_tiles: int, world: int, k: int = 8, seed: int = 0) -> tuple:
+    """(r, M): the 8x8 tiles t with t % M == r that rank 0 re-renders to
+    check the assembled image -- about k of them, spread over the image.  M
+    is the largest modulus <= n_tiles // k with M % world == 1, so the k
+    tiles r, r + M, ... belong to k consecutive ranks (tile t is rank
+    t % world's, distributed.py): a cyclic split over up to k GPUs has every
+    rank's share checked."""
+    m0 = max(1, n_tiles // max(1, k))
+    m = m0 - (m0 - 1) % max(1, world)
+    if m < 1:
+        m = 1
+    r = int(np.random.default_rng(seed).integers(0, m))
+    return r, m
+
+
+def tile_ids(width: int, height: int) -> np.ndarray:
+    """Global 8x8 tile id of every texel, [height][width] (pt_binned.h
+    pixel_of: tile g covers x in [(g % tiles_x) * 8, +8), y in [(g // tiles_x)
+    * 8, +8), tiles_x = ceil(width / 8))."""
+    tiles_x = -(-width // 8)
+    y, x = np.mgrid[0:height, 0:width]
+    return (y // 8) * tiles_x + (x // 8)
+
+
+def compare_tiles(img: np.ndarray, ref: np.ndarray, r: int, m: int) -> dict:
+    """Bit-for-bit comparison of the assembled image with a render of the
+    tiles t % m == r alone (ref: zero outside them, pt_set_tiles): every
+    texel of those tiles, all four channels, as bit patterns (NaN texels
+    included)."""
+    h, w = img.shape[:2]
+    ids = tile_ids(w, h)
+    sel = ids % m == r
+    a = img.view(np.uint32)[sel]
+    b = ref.view(np.uint32)[sel]
+    bad = int(np.count_nonzero((a != b).any(axis=-1)))
+    outside_zero = bool(not np.any(ref.view(np.uint32)[~sel]))
+    tiles = sorted(int(t) for t in np.unique(ids[sel]))
+    return {"tiles": tiles, "texels": int(np.count_nonzero(sel)), "mismatched_texels": bad,
+            "ref_zero_outside": outside_zero, "bit_exact": bad == 0 and outside_zero and bool(np.any(sel))}
+
+
+def validate_tiles(img: np.ndarray, prog, settings, width: int, height: int, device: int, frames: int,
+                   world: int, seed: int) -> dict:
+    """Rank 0's check of the assembled (reduced) image after the timed steps:
+    a fresh context renders ~8 tiles of the image -- pt_set_tiles(r, M), see
+    check_tiles_spec -- over every frame the run accumulated (frame 1 ..
+    frames, as TileSplitRender counts them, path_tracer.rs:110-111), and the
+    texels must equal the image's bit for bit (the texel of
+    test_compute.glsl:242-245 that the reduce's sum must preserve).  Cost:
+    ~8 x 64 pixels x frames samples."""
+    from compute_path_tracer_amd import _native as N
+    from compute_path_tracer_amd.path_tracer import PathTracer
+
+    n_tiles = -(-width // 8) * -(-height // 8)
+    r, m = check_tiles_spec(n_tiles, world, seed=seed)
+    t0 = time.perf_counter()
+    ref = PathTracer(width, height, prog, device=device, settings=settings)
+    try:
+        # the binned passes whatever the sample count (the automatic choice
+        # would give a one-rank run's ~4 M samples to the tile-resident
+        # kernel, whose ~9 waves would take seconds)
+        ref.set_option("kernel", "binned")
+        ref.set_tiles(r, m)
+        ref.dispatch(N.Constants(time=0.0, frame=1, aspect=float(np.float32(width) / np.float32(height)),
+                                 last_clear=1), frames)
+        want = ref.read_image()
+    finally:
+        ref.close()
+    out = compare_tiles(img, want, r, m)
+    out.update({"frames": frames, "modulus": m, "residue": r,
+                "owner_ranks": sorted({t % world for t in out["tiles"]}),
+                "check_s": round(time.perf_counter() - t0, 3)})
+    return out
+
+
+def validation_failures(out: dict) -> list:
+    """Why an N-GPU line must not be trusted (bench.py exits non-zero):
+    RCCL's communicator does not hold n_gpus ranks, or rank 0's tile check
+    (validate_tiles) or the full re-render (--validate) found a texel that
+    differs -- for the headline and for the c4_strong leg alike."""
+    bad = []
+    for name, o in (("headline", out), ("c4_strong", out.get("c4_strong"))):
+        if not o:
+            continue
+        n = o.get("n_gpus", 1)
+        if n > 1 and o.get("reduce_backend") == "rccl" and o.get("rccl_ranks") != n:
+            bad.append(f"{name}: RCCL communicator has {o.get('rccl_ranks')} ranks, n_gpus is {n}")
+        for key in ("tile_check", "validation"):
+            v = o.get(key)
+            if v is not None and not v.get("bit_exact"):
+                bad.append(f"{name}: {key} not bit-exact ({v.get('mismatched_texels', '?')} texels differ)")
+    return bad
+
+
+def rank_render_ms(dist, ms: float, device: str) -> dict:
+    """One dispatch's device time (HIP events on the rank's stream) over the
+    ranks: min / max and their ratio -- the cyclic tile split's load balance
+    (distributed.py)."""
+    lo = max_over_ranks(dist, ms, device, "MIN")
+    hi = max_over_ranks(dist, ms, device, "MAX")
+    return {"min": round(lo, 3), "max": round(hi, 3), "max_over_min": round(hi / lo, 4) if lo > 0 else None}
 
 
 def reduce_probe(tr, pt, barrier, dist, device: str, reps: int = 3) -> float:
@@ -373,8 +514,9 @@ def strong_leg(local_rank, rank, world, mode, barrier, dist, device, steps: int,
     from compute_path_tracer_amd.sdf_editor import CompData
 
     scene, w, h, spp, bounces = scenes.CONFIGS["c4"]
-    pt = PathTracer(w, h, scenes.SCENES[scene]().compile(CompData()), device=local_rank,
-                    settings=N.Settings(debug=0, bounces=bounces, scale=1.0, fov=1.0, aabb=0))
+    prog = scenes.SCENES[scene]().compile(CompData())
+    settings = N.Settings(debug=0, bounces=bounces, scale=1.0, fov=1.0, aabb=0)
+    pt = PathTracer(w, h, prog, device=local_rank, settings=settings)
     pt.set_option("jit_wait", 1)
     tr = TileSplitRender(pt, rank, world, float(np.float32(w) / np.float32(h)), reduce=mode, scaling="strong")
     rccl_ranks = pt.comm_size() if world > 1 and mode == "rccl" else None
@@ -390,13 +532,16 @@ def strong_leg(local_rank, rank, world, mode, barrier, dist, device, steps: int,
     pt.sync()
     barrier()
     dt = max_over_ranks(dist, time.perf_counter() - t0, device)
-    render_ms = max_over_ranks(dist, pt.last_dispatch_ms(), device)  # the last step's render on this rank's stream
+    render = rank_render_ms(dist, pt.last_dispatch_ms(), device)  # the last step's render on each rank's stream
     red = reduce_probe(tr, pt, barrier, dist, device)
+    img = tr.image(0)  # (every rank takes part in the reduce)
+    check = validate_tiles(img, prog, settings, w, h, local_rank, tr.frame - 1, world, seed=4) if rank == 0 else None
     pt.close()
     return {"metric": "Msamples/sec, BASELINE config 4 split over the GPUs",
             "value": round(w * h * spp * steps / dt / 1e6, 3), "unit": "Msamples/sec", "scaling": "strong",
             "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(dt * 1e3 / steps, 3),
-            "render_ms_max_rank": round(render_ms, 3), "reduce_ms": round(red, 3), "rccl_ranks": rccl_ranks,
+            "render_ms_max_rank": render["max"], "render_ms_per_rank": render, "reduce_ms": round(red, 3),
+            "rccl_ranks": rccl_ranks, "reduce_backend": mode, "tile_check": check,
             "config": {"workload": f"c3 {w}x{h}, {bounces} bounces, {spp} spp per step over all GPUs",
                        "width": w, "height": h, "bounces": bounces, "spp_per_step": spp,
                        "parallelism": f"tiles{world}", "reduce": "RCCL ncclReduce(sum) onto rank 0"
@@ -471,6 +616,11 @@ def main() -> None:
                     help="gloo + host image reduce: rehearsal with ranks sharing one GPU")
     ap.add_argument("--validate", action="store_true",
                     help="rank 0 re-renders every frame on one GPU and checks the assembled image bit for bit")
+    ap.add_argument("--no-tile-check", action="store_true",
+                    help="skip rank 0's default check of ~8 tiles of the assembled image against a fresh render")
+    ap.add_argument("--no-table-kernel", action="store_true",
+                    help="skip the one-GPU timing of the table scene kernel (jit_bake 0: what a value-editing "
+                         "session runs)")
     args = ap.parse_args()
     world, launch = resolve_world(args.gpus)
     if launch:
@@ -553,8 +703,11 @@ def main() -> None:
     barrier()
     kernel_ms, trace_ms, trace_n, shade_ms, shade_n = [], [], [], [], []
 
+    chunks = []
+
     def record_times():
         kernel_ms.append(pt.last_dispatch_ms())  # whole dispatch (all pipeline kernels)
+        chunks.append(int(pt.get_option("bin_chunks")))
         n = int(pt.get_option("trace_launches"))
         if n:  # binned pipeline: the trace / shade passes, timed by events on each pipeline's stream
             trace_ms.append(pt.get_option("trace_ms"))
@@ -574,18 +727,28 @@ def main() -> None:
         # per-launch kernel time on this rank (events on the library stream)
         tr.step(spp)
         record_times()
+    render = rank_render_ms(dist, kernel_ms[-1], dev)  # one step's dispatch on each rank
     reduce_ms = reduce_probe(tr, pt, barrier, dist, dev)
-    solo = solo_pipeline(pt, aspect, spp_step) if world == 1 and trace_n else None
+    # every frame rendered so far, assembled on rank 0 (all ranks take part
+    # in the reduce); checked there against a fresh render of ~8 tiles, and
+    # with --validate against a re-render of the whole image
+    img = tr.image(0)
+    tile_check = None
     validation = None
-    if args.validate:
-        img = tr.image(0)  # every frame rendered so far, assembled on rank 0
-        if rank == 0:
+    if rank == 0:
+        if not args.no_tile_check:
+            tile_check = validate_tiles(img, prog, settings, width, height, local_rank, tr.frame - 1, world, seed=3)
+        if args.validate:
             ref = PathTracer(width, height, prog, device=local_rank, settings=settings)
             ref.dispatch(N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1), tr.frame - 1)
             want = ref.read_image()
             validation = {"frames": tr.frame - 1,
                           "bit_exact": bool(np.array_equal(img.view(np.uint32), want.view(np.uint32)))}
             ref.close()
+    # (after the checks: the solo and table-kernel runs overwrite the image)
+    solo = solo_pipeline(pt, aspect, spp_step) if world == 1 and trace_n else None
+    table = table_kernel_leg(pt, prog, aspect, spp_step) if world == 1 and trace_n and not args.no_table_kernel \
+        else None
 
     pixels = width * height
     samples_step = pixels * spp * (world if scaling == "weak" else 1)  # all ranks
@@ -596,8 +759,13 @@ def main() -> None:
     if rank == 0:
         out = report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, spp_step, world, scaling,
                      value, ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation,
-                     solo)
+                     solo, chunks)
         out["rccl_ranks"] = rccl_ranks
+        out["reduce_backend"] = mode if world > 1 else None
+        out["render_ms_per_rank"] = render
+        out["tile_check"] = tile_check
+        if table is not None:
+            out["table_kernel"] = table
     pt.close()
     if world > 1 and scaling == "weak" and args.c4_steps > 0 and not args.validate:
         leg = strong_leg(local_rank, rank, world, mode, barrier, dist, dev, args.c4_steps, 1)
@@ -608,12 +776,28 @@ def main() -> None:
     if dist is not None:
         barrier()
         dist.destroy_process_group()
+    rc = exit_status(out)
+    if rc:
+        sys.exit(rc)
+
+
+def exit_status(out) -> int:
+    """bench.py's exit status once the line is printed: 1 (with the reasons
+    on stderr) when validation_failures finds any, else 0.  Ranks other than
+    0 hold no line (None) and exit 0."""
+    fails = validation_failures(out) if out is not None else []
+    if fails:
+        print("bench.py: the line is NOT valid: " + "; ".join(fails), file=sys.stderr, flush=True)
+        return 1
+    return 0
 
 
 def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, spp_step, world, scaling, value,
-           ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation, solo=None) -> dict:
+           ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation, solo=None,
+           chunks=None) -> dict:
     """Rank 0's JSON line."""
     d_ms = float(np.mean(kernel_ms))  # one dispatch = one step's frames of this rank
+    n_chunks = float(np.mean(chunks)) if chunks else 1.0  # binned chunks per dispatch
     flops_step = algorithmic_flops(st)
     rank_pixels = st["samples"] / max(1, spp_step)
     image_bytes = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per dispatch
@@ -696,7 +880,14 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
                                   else f"{spp} spp per step over all GPUs") + ", progressive accumulate",
                    "width": width, "height": height, "bounces": bounces,
                    "spp_per_step": spp * world if scaling == "weak" else spp, "parallelism": f"tiles{world}",
-                   "pipelines": int(pt.get_option("bin_lanes")), "baseline_config": args.config},
+                   "pipelines": int(pt.get_option("bin_lanes")), "baseline_config": args.config,
+                   "scene_kernel": "values-baked tier (jit_bake 2 tier-up, installed before timing; the table "
+                                   "kernel an editing session runs between value edits: table_kernel)"
+                                   if jit and pt.get_option("jit_tier_active") else
+                                   ("table scene kernel" if jit else "op-list interpreter"),
+                   # chunking (pt_runtime.hip bin_samples: fixed per context from the device's total memory)
+                   "bin_samples": int(pt.get_option("bin_samples")), "chunks_per_dispatch": n_chunks,
+                   "bin_fallback": bool(pt.get_option("bin_fallback"))},
         "roofline": {"bound": "valu",
                      "bound_note": "FP32 vector ALU: no dense contraction on this path, so no MFMA, and arithmetic "
                                    "intensity ~65 flop/B of measured traffic is above the HBM ridge; the metric's "
@@ -766,18 +957,31 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
         # on the pipeline's own access shapes: scripts/summarize_profile.py)
         # next to the same kernel's algorithmic bytes per launch
         lanes = int(pt.get_option("bin_lanes"))
-        n_first = float(lanes)  # one first pass (pt_bin_trace_g_jit) per pipeline per step
+        # one first pass (pt_bin_trace_g_jit) per pipeline per chunk
+        n_first = float(lanes) * n_chunks
         n_march = max(1.0, float(np.mean(trace_n)) - n_first)
         # the profile ran one pipeline: a launch there carries `lanes` times
         # the frames of a launch here
         scale = float(pd["bench_config"].get("pipelines", 1)) / float(lanes)
         tk = pk.get(hot) or {}
         if "hbm_bytes_per_launch" in tk:
-            out["roofline"]["traffic"] = round(tk["hbm_bytes_per_launch"] * scale)
-            out["roofline"]["traffic_source"] = (f"{src} (one pipeline, scaled to this run's launch size): "
-                                                 f"FETCH_SIZE + WRITE_SIZE (KiB -> B) per {hot} launch; "
-                                                 "profiles/r04q_calib_traffic.json: the counters are exact for its "
-                                                 "64 B record gathers and stores")
+            # per access shape (profiles/r04q_calib_traffic.json): FETCH_SIZE
+            # counts the 64 B record gathers at 1.00 of their bytes; WRITE_SIZE
+            # counts the march pass's only stores, 16 B hit quads at scattered
+            # binned positions, at 2.00 (a 32 B granule moves), so the
+            # corrected figure halves the writes.  The 4 B slot reads (6 % of
+            # the bytes) are left as counted.
+            fetch, write = tk.get("fetch_bytes_per_launch"), tk.get("write_bytes_per_launch")
+            if fetch is not None and write is not None and hot == "pt_bin_trace_m_jit":
+                out["roofline"]["traffic"] = round((fetch + 0.5 * write) * scale)
+                out["roofline"]["traffic_uncorrected"] = round(tk["hbm_bytes_per_launch"] * scale)
+                corr = "FETCH_SIZE + WRITE_SIZE / 2 (the 16 B scattered hit-quad stores count twice)"
+            else:
+                out["roofline"]["traffic"] = round(tk["hbm_bytes_per_launch"] * scale)
+                corr = "FETCH_SIZE + WRITE_SIZE, uncorrected"
+            out["roofline"]["traffic_source"] = (f"{src} (one pipeline, scaled to this run's launch size): {corr}, "
+                                                 f"KiB -> B, per {hot} launch; calibration of the counters on the "
+                                                 "pipeline's access shapes: profiles/r04q_calib_traffic.json")
             out["roofline"]["traffic_algorithmic"] = round(pipe["trace_m"] / n_march)
         first = pk.get("pt_bin_trace_g_jit") or {}
         if gen_trace and "hbm_bytes_per_launch" in first:
@@ -786,7 +990,10 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
                                                      "algorithmic": round(pipe["trace_first"] / n_first)}
         sk = pk.get(shade["kernel"]) if shade else None
         if sk and "hbm_bytes_per_launch" in sk:
+            # uncorrected: its 16 B coalesced quad reads count half, its
+            # scattered 16 B colour updates twice (r04q_calib_traffic.json)
             out["roofline"]["shade"]["traffic"] = round(sk["hbm_bytes_per_launch"] * scale)
+            out["roofline"]["shade"]["traffic_note"] = "FETCH_SIZE + WRITE_SIZE, uncorrected"
             out["roofline"]["shade"]["traffic_algorithmic"] = round(pipe["shade"] / max(1.0, float(np.mean(shade_n))))
         out["hbm"]["trace_kernel_measured_bytes_per_launch"] = out["roofline"].get("traffic")
         if tk:

@@ -675,7 +675,8 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                 r[2] = make_uint4(__float_as_uint(s2.x), __float_as_uint(s2.y), __float_as_uint(s2.z),
                                   __float_as_uint(s2.w));
                 r[3] = s3;
-                if (wide_of<Map>(P)) P.mask_hi[wbase + uint32_t(lane)] = sh;
+                // (check[] bits 64..127 need no copy here: the shade pass
+                // takes a hit's from its hitn entry, P.hitn)
             }
         }
         in_lds = true;

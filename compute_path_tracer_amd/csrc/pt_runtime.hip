@@ -76,6 +76,8 @@ struct pt_ctx {
     int jit_bake = 2;             // 0 values from the node table, 1 baked as literals, 2 tier-up
     int bin_samples = 0;          // binned pipeline: samples per chunk; 0 = automatic (bin_samples())
     size_t bin_auto = 0;          // the automatic chunk size, fixed at the first binned dispatch
+    bool bin_fallback = false;    // bin_auto came from the free memory (the total-memory size did not fit)
+    uint32_t last_chunks = 0;     // chunks of the last timed binned dispatch
     PtJitModule jit_mod;   // scene kernel for the topology (key = its source)
     // tier-up (jit_bake 2): the same kernel with the current values baked in as
     // literals, compiled on a worker thread and used once ready while the
@@ -634,24 +636,41 @@ static size_t bin_bytes_per_sample(const pt_ctx *c) {
 // Samples per chunk: pt_set_option "bin_samples", else automatic: 2^29 (a
 // whole 256-spp 1080p render: 90 GB of HBM at 168 B per sample; every pass's
 // tail is paid once per chunk, so larger chunks are faster: 64 -> 256 frames
-// per chunk +5 %), at most half of what this context could hold on its
-// device -- the free memory plus the chunk buffers it already owns (other
-// contexts' allocations count as used, so several ranks sharing one GPU each
-// size to what is left).  The automatic size is fixed at the context's first
-// binned dispatch, so a workload chunks the same way on every later one
-// whatever other allocations come and go.  The caller's current device is
-// left as it was.
-static size_t bin_samples(pt_ctx *c) {
-    if (c->bin_samples > 0) return size_t(c->bin_samples);
-    if (c->bin_auto) return c->bin_auto;
-    const size_t per = bin_bytes_per_sample(c);
-    size_t free_b = 0, total_b = 0;
+// per chunk +5 %), at most half of the device's TOTAL memory.  The total,
+// not the free memory: a torch-first process's caching allocator moves the
+// free figure, and every rank of a multi-GPU run must chunk its share the
+// same way whatever else it holds.  Only when the
+// chunk buffers then do not fit (several contexts sharing one GPU) does the
+// size fall back to half of what this context could hold -- the free
+// memory plus the buffers it already owns (bin_samples_free; launch_binned).
+// The automatic size is fixed at the context's first binned dispatch.  The
+// caller's current device is left as it was.
+static bool device_mem(const pt_ctx *c, size_t &free_b, size_t &total_b) {
+    free_b = total_b = 0;
     int prev = -1;
     const bool have_prev = hipGetDevice(&prev) == hipSuccess;
     const bool ok = hipSetDevice(c->device) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
                     total_b != 0;
     if (have_prev) (void)hipSetDevice(prev);
-    if (!ok) return size_t(1) << 27;
+    return ok;
+}
+
+static size_t bin_samples(pt_ctx *c) {
+    if (c->bin_samples > 0) return size_t(c->bin_samples);
+    if (c->bin_auto) return c->bin_auto;
+    size_t free_b = 0, total_b = 0;
+    if (!device_mem(c, free_b, total_b)) return size_t(1) << 27;
+    const size_t cap = std::max<size_t>(size_t(1) << 20, total_b / 2 / bin_bytes_per_sample(c));
+    return std::min<size_t>(size_t(1) << 29, cap);
+}
+
+// The fallback when bin_samples()'s chunk buffers did not fit: half of the
+// free memory plus what this context holds (other contexts' allocations
+// count as used, so ranks sharing one GPU each size to what is left).
+static size_t bin_samples_free(pt_ctx *c) {
+    const size_t per = bin_bytes_per_sample(c);
+    size_t free_b = 0, total_b = 0;
+    if (!device_mem(c, free_b, total_b)) return size_t(1) << 27;
     const size_t held = c->bin_cap * size_t(c->n_lanes) * per;
     const size_t cap = std::max<size_t>(size_t(1) << 20, (free_b + held) / 2 / per);
     return std::min<size_t>(size_t(1) << 29, cap);
@@ -762,12 +781,27 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         spp = 1;
     }
     if (!c->bin_samples && !c->bin_auto) c->bin_auto = bin_samples(c);  // (fixed from now on)
-    const uint32_t F = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, bin_samples(c) / n_pix)));
     const int passes = L.bounces + 1;
-    const int lanes = int(std::min<uint32_t>(uint32_t(c->bin_lanes), F));
-    const uint32_t FL = (F + uint32_t(lanes) - 1) / uint32_t(lanes);  // frames per lane
+    uint32_t F = 0, FL = 0;
+    int lanes = 0;
+    auto size_chunk = [&]() {
+        F = uint32_t(std::max<size_t>(1, std::min<size_t>(spp, bin_samples(c) / n_pix)));
+        lanes = int(std::min<uint32_t>(uint32_t(c->bin_lanes), F));
+        FL = (F + uint32_t(lanes) - 1) / uint32_t(lanes);  // frames per lane
+    };
+    size_chunk();
     int rc = ensure_bin(c, size_t(n_pix) * FL, size_t(passes), lanes);
+    if (rc == PT_ERR_HIP && !c->bin_samples && !c->bin_fallback) {
+        // the total-memory size does not fit (contexts sharing the GPU):
+        // size to the free memory once, fixed from now on
+        c->bin_fallback = true;
+        c->bin_auto = bin_samples_free(c);
+        c->err.clear();
+        size_chunk();
+        rc = ensure_bin(c, size_t(n_pix) * FL, size_t(passes), lanes);
+    }
     if (rc != PT_OK) return rc;
+    if (!stats) c->last_chunks = (spp + F - 1) / F;
     const unsigned cu = unsigned(std::max(1, c->cu_count));
     auto item_grid = [&](size_t n) {
         return unsigned(std::max<size_t>(1, std::min<size_t>((n + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK, 4 * cu)));
@@ -1268,6 +1302,8 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "kernel")) *value = c->kernel;
     else if (!std::strcmp(key, "shade_batch")) *value = c->shade_batch;
     else if (!std::strcmp(key, "bin_samples")) *value = double(bin_samples(c));
+    else if (!std::strcmp(key, "bin_chunks")) *value = double(c->last_chunks);  // of the last timed binned dispatch
+    else if (!std::strcmp(key, "bin_fallback")) *value = c->bin_fallback ? 1.0 : 0.0;
     else if (!std::strcmp(key, "trace_launches")) *value = double(c->tlog.used / 2);
     else if (!std::strcmp(key, "shade_launches")) *value = double(c->slog.used / 2);
     else if (!std::strcmp(key, "display_ms")) {

@@ -232,7 +232,9 @@ int pt_display(pt_ctx *ctx, int format, void *out, size_t bytes);
  * wait before a shading pass runs, 1..64), "bin_samples" (binned kernel:
  * samples per chunk, >= 64; device memory = 168 B per sample, 192 B for
  * scenes with > 64 check[] entries; default 2^29 samples, at most half of
- * the device memory this context could hold), "bin_lanes"
+ * the device's total memory -- or, when that does not fit beside other
+ * contexts on the same GPU, half of what this context could hold -- fixed at
+ * the context's first binned dispatch), "bin_lanes"
  * (binned kernel: 1..4 pipelines, each on its own stream, over which a
  * chunk's frames are split, so one's memory-bound passes overlap another's
  * trace pass), "jit" (1:
@@ -250,7 +252,8 @@ int pt_set_option(pt_ctx *ctx, const char *key, int value);
  * "jit_tier_seconds" (values-baked build in use / its compile time),
  * "kernel", "shade_batch",
  * "bin_samples", "bin_lanes", "bin_bytes" (device memory held by the binned
- * pipeline), "trace_ms" / "trace_launches" (device time and count of the last
+ * pipeline), "bin_chunks" (chunks of the last binned dispatch), "bin_fallback"
+ * (1: the chunk size came from the free memory), "trace_ms" / "trace_launches" (device time and count of the last
  * dispatch's binned trace passes, HIP events on each pipeline's stream),
  * "shade_ms" / "shade_launches" (the same for its shade passes), "display_ms"
  * (device time of the last pt_display's kernel). */

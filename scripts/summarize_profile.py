@@ -13,10 +13,14 @@ pipeline's own shapes were calibrated with known-byte probes (pt_probe.hip,
 profiles/r04q_calib_traffic.json): a 64 B record gathered by slot reads
 FETCH_SIZE = its bytes (ratio 1.0), a 64 B record store WRITE_SIZE = its
 bytes, a 16 B store at a scattered position WRITE_SIZE = 2x (a 32 B write
-granule moved), a 16 B/lane coalesced read FETCH_SIZE = half.  The trace
-and shade passes' traffic is dominated by the exact shapes (64 B gathers and
-stores), so the sum is used as is: what the memory side moved, up to the
-coalesced 16 B reads' undercount (the shade pass's hit quads, the slot list).
+granule moved), a 16 B/lane coalesced read FETCH_SIZE = half.  The sums
+here are the raw counters.  They are not exact for every kernel: the march
+pass's (pt_bin_trace_m_jit) only stores are 16 B hit quads at scattered
+positions, which WRITE_SIZE counts twice, so bench.py reports its traffic as
+FETCH_SIZE + WRITE_SIZE / 2 (fetch_bytes_per_launch and
+write_bytes_per_launch are kept apart for that); the shade pass mixes
+shapes (coalesced 16 B quad reads counted half, scattered 16 B colour
+updates twice, exact 64 B gathers and stores) and is left uncorrected.
 The hot kernel is the binned trace pass when present (averages over its
 launches), else the tile-resident kernel; every kernel's figures are in
 per_kernel.

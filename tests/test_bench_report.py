@@ -133,6 +133,35 @@ def test_profiled_traffic_scaled_to_the_launch(frame, tmp_path, monkeypatch):
     assert r["hw"]["valu_lane_slots_busy"] == pytest.approx(0.4)
 
 
+def test_march_traffic_halves_the_scattered_quad_writes(frame, tmp_path, monkeypatch):
+    """The march pass's only stores are 16 B hit quads at scattered
+    positions, which WRITE_SIZE counts twice (r04q_calib_traffic.json):
+    roofline.traffic = FETCH_SIZE + WRITE_SIZE / 2, the raw sum kept beside
+    it; and with two chunks per dispatch there are two first
+    passes per pipeline."""
+    out0 = _report(frame)
+    cfg = {k: out0["config"][k] for k in ("width", "height", "bounces", "spp_per_step", "workload")}
+    pmc = {"bench_config": dict(cfg, pipelines=1),
+           "per_kernel": {"pt_bin_trace_m_jit": {"hbm_bytes_per_launch": 1400.0, "fetch_bytes_per_launch": 1000.0,
+                                                 "write_bytes_per_launch": 400.0},
+                          "pt_bin_trace_g_jit": {"hbm_bytes_per_launch": 4000.0}}}
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "zz_pmc.json").write_text(json.dumps(pmc))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    ed, prog, st, taps = frame
+    solo = {"frames": 1, "st": st, "taps": taps, "dispatch_ms": 2.0, "trace_ms": 1.5, "trace_n": 9,
+            "shade_ms": 0.5, "shade_n": 9}
+    out = bench.report(_Args, _Ctx(), st, taps, prog, "c3", W, H, 8, SPP, SPP, 1, "weak", 1.0, 3.0, [3.0],
+                       [2.0], [18], [1.0], [18], 0.0, ed, None, solo, [2])
+    r = json.loads(json.dumps(out))["roofline"]
+    assert r["traffic"] == 600 and r["traffic_uncorrected"] == 700  # (1000 + 200, 1400) x 1/2 pipelines
+    assert "WRITE_SIZE / 2" in r["traffic_source"]
+    pipe = bench.pipeline_bytes(st, W * H, gen_trace=True)
+    assert r["traffic_algorithmic"] == round(pipe["trace_m"] / 14)  # 18 launches less 2 x 2 first passes
+    assert r["traffic_first_pass"]["algorithmic"] == round(pipe["trace_first"] / 4)
+    assert out["config"]["chunks_per_dispatch"] == 2.0
+
+
 def test_launch_split(tmp_path):
     """summarize_profile.launch_split: the last n launches of each pass are
     bench.py's solo dispatch, the rest its timed steps."""

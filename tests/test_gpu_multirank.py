@@ -49,6 +49,56 @@ def test_two_ranks_tile_split_bit_exact(gpu, config, scaling):
     frames = (1 + 2 + 1) * 4 * (2 if scaling == "weak" else 1)  # warm-up, timed steps, the per-launch timing step
     assert out["validation"] == {"frames": frames, "bit_exact": True}
     assert out["reduce_ms"] > 0 and out["value"] > 0
+    # the default tile check agrees, and covers both ranks' tiles
+    tc = out["tile_check"]
+    assert tc["bit_exact"] is True and tc["frames"] == frames and tc["owner_ranks"] == [0, 1]
+
+
+@pytest.mark.timeout(600)
+def test_default_line_checks_its_tiles(gpu):
+    """Without --validate the N > 1 line still proves itself (VERDICT r04
+    item 1): rank 0 re-renders ~8 tiles over every accumulated frame and
+    compares the assembled image bit for bit; per-rank render times give the
+    tile split's balance; the c4_strong leg carries the same check."""
+    out = _bench("--width", "480", "--height", "272", "--spp", "4", "--steps", "2", "--warmup", "1",
+                 "--c4-steps", "1")
+    tc = out["tile_check"]
+    assert tc["bit_exact"] is True and tc["mismatched_texels"] == 0 and tc["ref_zero_outside"]
+    assert tc["frames"] == (1 + 2 + 1) * 4 * 2 and tc["owner_ranks"] == [0, 1] and len(tc["tiles"]) >= 8
+    pr = out["render_ms_per_rank"]
+    assert 0 < pr["min"] <= pr["max"] and pr["max_over_min"] >= 1.0
+    assert out["reduce_backend"] == "host" and "validation" not in out
+    leg = out["c4_strong"]
+    assert leg["tile_check"]["bit_exact"] is True and leg["tile_check"]["frames"] == 2 * 256
+    assert leg["render_ms_per_rank"]["max"] == leg["render_ms_max_rank"]
+    assert bench_exit_ok(out)
+
+
+def bench_exit_ok(out: dict) -> bool:
+    sys.path.insert(0, ROOT)
+    import bench
+
+    return bench.validation_failures(out) == []
+
+
+@pytest.mark.timeout(600)
+def test_one_gpu_validate_and_tile_check(gpu):
+    """bench.py --validate on ONE rank (the solo-pipeline run
+    had overwritten the image before the check): both checks bit-exact, and
+    the table scene kernel's throughput on the line."""
+    # (32 spp: enough samples per step for the binned pipeline, whose
+    # solo-pipeline run used to overwrite the image)
+    cmd = [sys.executable, "-u", "bench.py", "--no-cpu-baseline", "--width", "480", "--height", "272", "--spp", "32",
+           "--steps", "2", "--warmup", "1", "--validate"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=500)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["n_gpus"] == 1
+    assert out["validation"] == {"frames": (1 + 2) * 32, "bit_exact": True}
+    assert out["tile_check"]["bit_exact"] is True and out["tile_check"]["frames"] == 96
+    assert out["roofline"]["kernel"] == "pt_bin_trace_m_jit"
+    assert out["table_kernel"]["value"] > 0 and out["config"]["chunks_per_dispatch"] == 1.0
 
 
 @pytest.mark.timeout(600)
