@@ -322,7 +322,11 @@ def solo_pipeline(pt, aspect: float, frames_step: int) -> dict:
     chunk = max(1, min(frames_step, int(pt.get_option("bin_samples")) // n_pix))  # frames per chunk
     frames = -(-chunk // lanes)  # one pipeline's share of a chunk: the buffers fit as they are
     c = N.Constants(time=0.0, frame=1, aspect=aspect, last_clear=1)
+    kernel = int(pt.get_option("kernel"))
     pt.set_option("bin_lanes", 1)
+    # the binned passes even when one pipeline's share is small enough for
+    # the automatic choice to take the tile-resident kernel
+    pt.set_option("kernel", "binned")
     try:
         st = pt.stats(c, frames)
         taps = pt.tap_stats()
@@ -333,6 +337,7 @@ def solo_pipeline(pt, aspect: float, frames_step: int) -> dict:
                 "shade_ms": pt.get_option("shade_ms"), "shade_n": int(pt.get_option("shade_launches"))}
     finally:
         pt.set_option("bin_lanes", lanes)
+        pt.set_option("kernel", kernel)
 
 
 def table_kernel_leg(pt, prog, aspect: float, frames: int, steps: int = 2) -> dict:

@@ -47,7 +47,7 @@ SYMBOLS = (
     "pt_dispatch_stats", "pt_set_option", "pt_get_option", "pt_jit_log", "pt_jit_compile", "pt_last_error",
     "pt_destroy", "pt_abi_version", "pt_device_math", "pt_check_sqrt_exhaustive", "pt_check_div_exhaustive",
     "pt_check_div_random", "pt_check_box_random", "pt_check_div_k", "pt_display", "pt_write_accum",
-    "pt_compile_scene_keyed", "pt_save_rgba8", "pt_comm_size", "pt_traffic_probe",
+    "pt_compile_scene_keyed", "pt_save_rgba8", "pt_comm_size", "pt_traffic_probe", "pt_scene_kernel_source",
 )
 PT_MATH = {"max": 0, "min": 1, "sqrt": 2, "sqrtf": 3, "sin": 4, "cos": 5, "div": 6, "fma": 7}
 
@@ -149,6 +149,8 @@ def lib() -> ctypes.CDLL:
         "pt_jit_log": (c_char_p, [ctx]),
         "pt_jit_compile": (c_int, [POINTER(Op), c_uint32, POINTER(Aabb), c_uint32, POINTER(c_float), c_uint32, c_char_p,
                                    c_size_t, POINTER(c_size_t)]),
+        "pt_scene_kernel_source": (c_int, [POINTER(Op), c_uint32, POINTER(Aabb), c_uint32, POINTER(c_float), c_uint32,
+                                           c_int, c_char_p, c_size_t, POINTER(c_size_t)]),
         "pt_last_error": (c_char_p, [ctx]),
         "pt_destroy": (None, [ctx]),
         "pt_abi_version": (c_int, []),

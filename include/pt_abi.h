@@ -264,6 +264,13 @@ const char *pt_jit_log(const pt_ctx *ctx);
  * a device (validation / cache warm-up); *code_bytes = code object size. */
 int pt_jit_compile(const pt_op *ops, uint32_t n_ops, const pt_aabb *aabbs, uint32_t n_aabb, const float *data,
                    uint32_t n_data, char *log, size_t log_cap, size_t *code_bytes);
+/* The scene kernel source pt_jit_compile would build for (program, data),
+ * without compiling it (the counterpart of the reference's spliced-shader dump
+ * shader_out/test_compute.glsl, glsl_preprocessor.rs:5-15).  baked != 0: node
+ * values as literals (the tier-up build).  Host only; two-call pattern, *len
+ * includes the terminating NUL. */
+int pt_scene_kernel_source(const pt_op *ops, uint32_t n_ops, const pt_aabb *aabbs, uint32_t n_aabb,
+                           const float *data, uint32_t n_data, int baked, char *out, size_t cap, size_t *len);
 const char *pt_last_error(const pt_ctx *ctx);
 void pt_destroy(pt_ctx *ctx);
 int pt_abi_version(void);

@@ -23,6 +23,9 @@ rc = N.lib().pt_jit_compile(prog.ops, prog.n_ops, prog.aabbs, prog.n_aabb,
                             prog.data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(prog.data), log, len(log),
                             None)
 assert rc == 0, log.value.decode()
+for l in log.value.decode().splitlines():
+    if l.startswith("(rebuilt"):
+        print(l)
 llvm = "/opt/rocm/lib/llvm/bin"
 dis = subprocess.run([f"{llvm}/llvm-objdump", "-d", "--mcpu=gfx950", os.environ["PT_JIT_CODE_DUMP"]],
                      capture_output=True, text=True).stdout

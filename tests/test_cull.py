@@ -34,23 +34,18 @@ def _value(tok: str) -> float:
 
 
 def _baked(scene: str, tmp_path):
+    """The values-baked scene kernel source (pt_scene_kernel_source: generated,
+    not compiled) and its node literals."""
     prog = scenes.SCENES[scene]().compile(CompData())
-    dump = tmp_path / f"{scene}.hip"
-    old = {k: os.environ.get(k) for k in ("PT_JIT_BAKE", "PT_JIT_DUMP")}
-    os.environ["PT_JIT_BAKE"], os.environ["PT_JIT_DUMP"] = "1", str(dump)
-    try:
-        log = ctypes.create_string_buffer(1 << 16)
-        rc = N.lib().pt_jit_compile(prog.ops, prog.n_ops, prog.aabbs, prog.n_aabb,
-                                    prog.data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(prog.data), log,
-                                    len(log), None)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    assert rc == N.PT_OK, log.value.decode()
-    src = dump.read_text()
+    args = (prog.ops, prog.n_ops, prog.aabbs, prog.n_aabb, prog.data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+            len(prog.data), 1)
+    n = ctypes.c_size_t()
+    assert N.lib().pt_scene_kernel_source(*args, None, 0, ctypes.byref(n)) == N.PT_OK
+    buf = ctypes.create_string_buffer(n.value)
+    assert N.lib().pt_scene_kernel_source(*args, buf, n.value - 1, ctypes.byref(n)) == N.PT_ERR_SIZE
+    assert N.lib().pt_scene_kernel_source(*args, buf, n.value, ctypes.byref(n)) == N.PT_OK
+    src = buf.value.decode()
+    assert len(src) + 1 == n.value
     nodes = []
     # the node literals of the first map (JitMap); JitMapB repeats them
     for m in re.finditer(r"constexpr PtNode B(\d+)\{(.*?)\};\n", src[:src.index("struct JitMapB")]):
