@@ -7,7 +7,9 @@ TAG="${PROF_TAG:-r01}"
 OUT="${GPU_OUT:-$R/gpurun_out}/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="${PROF_ARGS:---steps 4 --warmup 1 --no-cpu-baseline}"
+# (no tile check, no table-kernel leg: their launches carry the same kernel
+# names and would mix into the per-kernel statistics)
+ARGS="${PROF_ARGS:---steps 4 --warmup 1 --no-cpu-baseline} --no-tile-check --no-table-kernel"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
     python3 "$R/bench.py" $ARGS > "$OUT/kt_bench.log" 2>&1
 rc=$?; echo "kernel-trace rc=$rc"; tail -1 "$OUT/kt_bench.log"
@@ -18,7 +20,7 @@ if [ "${1:-}" = "pmc" ]; then
   for p in "${PASSES[@]}"; do
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $p --kernel-trace -d "$OUT/pmc$i" -o pmc --output-format csv -- \
-        python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline ${PMC_ARGS:-} > "$OUT/pmc${i}.log" 2>&1
+        python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-tile-check --no-table-kernel ${PMC_ARGS:-} > "$OUT/pmc${i}.log" 2>&1
     rc=$?; echo "pmc pass $i ($p) rc=$rc"
     [ $rc -eq 0 ] || exit $rc
   done
