@@ -166,6 +166,8 @@ def schedule_metrics(st_all: dict, taps: dict) -> dict:
                              "lane_evals_per_map": round((taps["xform_shape"] - taps["culled"]) / taps["normal_maps"], 3),
                              "wave_shapes_per_map": round(taps["wave_shapes"] / max(1, taps["wave_maps"]), 3),
                              "wave_evals_per_map": round(taps["wave_evals"] / max(1, taps["wave_maps"]), 3)}
+    if st.get("wave_maps"):  # wave-level map() evaluations of the trace passes (per-map instruction budgets)
+        out["trace_wave_maps"] = st["wave_maps"]
     if st.get("wave_shapes"):
         out["map_lane_util"] = round(st["xform_shape"] / (64.0 * st["wave_shapes"]), 4)
         out["wave_shapes_per_map"] = round(st["wave_shapes"] / max(1, st["wave_maps"]), 3)
