@@ -78,7 +78,10 @@ def main() -> None:
     if len(sys.argv) > 4:
         pmc = json.load(open(sys.argv[3]))
         maps = float(sys.argv[4])
-        c = pmc["per_launch_counters"] if pmc.get("kernel") == name else pmc["per_kernel"][name]
+        hot = pmc.get("kernel") or {}
+        if hot.get("kernel") != name:
+            raise SystemExit(f"{sys.argv[3]} holds raw counters for {hot.get('kernel')}, not {name}")
+        c = pmc["per_launch_counters"]
         per = {k: c[k] / maps for k in c if k.startswith("SQ_INSTS")}
         v = per.get("SQ_INSTS_VALU", 0.0)
         known = {k.replace("SQ_INSTS_VALU_", "").lower(): per.get(k, 0.0) for k in
