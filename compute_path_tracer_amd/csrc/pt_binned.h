@@ -182,7 +182,82 @@ struct MapBounds {
     static __device__ __forceinline__ uint4 mask(const PtLaunch &L, const pt_f3 &ro, const pt_f3 &rd, Stats<ST> &st) {
         return bounds_mask<ST>(L, ro, rd, st);
     }
+    // the same with box k's slab test skipped where bit k of `skip` is set
+    // (primary_box_skip: every lane of the wave provably misses box k); the
+    // generic loop ignores the hint
+    template <bool ST>
+    static __device__ __forceinline__ uint4 mask_skip(const PtLaunch &L, const pt_f3 &ro, const pt_f3 &rd, uint64_t skip,
+                                                      Stats<ST> &st) {
+        (void)skip;
+        return bounds_mask<ST>(L, ro, rd, st);
+    }
 };
+
+// The boxes that no lane of a wave can hit, for the first pass's camera rays
+// (DESIGN.md 3.20): bit k set = box k's fast-path slab test would report a
+// decided miss in every lane, so bounds() may skip it.  The rays of a window
+// (one 8x8 tile of one frame) share the camera's origin o and have nearly
+// the same direction, and a box is tested against the wave's whole bundle at
+// once, one box per lane: with y_a = RN(1/d_a) of every lane inside
+// [ylo_a, yhi_a] (one sign) and C = RN(b - o) a constant, each lane's slab
+// value RN(C * y_a) lies between the products at the interval's ends (RN is
+// monotone, so is the product in y for a fixed C).  Hence every lane's
+// tnear' >= L (the largest over the axes of the least corner product) and
+// tfar' <= U (the least of the largest).  U <= 0: tfar' <= 0 in every lane,
+// and the IEEE tfar has tfar''s sign (3.14): a miss.  L, U > 0 with
+// bits(L) - bits(U) > PT_ULP_MARGIN: every lane's slab gap exceeds the
+// margin, so its fast-path result is decided (3.19) and is a miss.  Either
+// way the lane's bit is 0 and the box does not change whether the lane takes
+// the exact fallback (its gap is above the margin).  Every lane of the wave
+// must be active; lanes outside the fast path's guards do not count (they
+// take the IEEE loop).  Returns 0 (skip nothing) unless the fast-path lanes
+// share one origin, the scene's boxes pass the guards and there are <= 64.
+__device__ __forceinline__ uint64_t primary_box_skip(const PtLaunch &L, const pt_f3 &ro, const pt_f3 &rd) {
+    const int nb = L.n_aabb;
+    if (L.fast_bounds == 0 || nb <= 0 || nb > 64) return 0ull;
+    const bool fast = pt_div_coord_ok(ro.x) && pt_div_coord_ok(ro.y) && pt_div_coord_ok(ro.z) &&
+                      pt_div_dir_ok(rd.x) && pt_div_dir_ok(rd.y) && pt_div_dir_ok(rd.z);
+    const uint64_t fm = __ballot(fast);
+    if (fm == 0ull) return 0ull;
+    // the origin of the first fast lane, and no fast lane with another one
+    const int l0 = __builtin_ctzll(fm);
+    const float ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ro.x), l0));
+    const float oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ro.y), l0));
+    const float oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ro.z), l0));
+    if (__ballot(fast && (__float_as_uint(ro.x) != __float_as_uint(ox) || __float_as_uint(ro.y) != __float_as_uint(oy) ||
+                          __float_as_uint(ro.z) != __float_as_uint(oz))) != 0ull)
+        return 0ull;
+    const float inf = __builtin_inff();
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool mine = lane < uint32_t(nb);  // lane k tests box k against the whole bundle
+    // (the offset through an empty asm: a per-lane address the compiler
+    // hoisted out of the persistent loop took two registers and spilled)
+    static_assert(sizeof(PtAabb) == 32, "box stride");
+    uint32_t off;
+    __asm__ volatile("v_lshlrev_b32 %0, 5, %1" : "=v"(off) : "v"(lane));
+    const float *box = reinterpret_cast<const float *>(reinterpret_cast<const char *>(L.aabbs) + off);
+    float lo = -inf, hi = inf;
+    // one axis at a time (few registers live): the lanes' y = the reciprocal
+    // bounds() itself forms (the same correctly rounded division), its wave
+    // range, and box k's corner products; an axis whose lanes' y straddle
+    // zero gives no finite bound and is left out
+    auto axis = [&](int a, float d, float o) {
+        const float y = 1.0f / d;
+        const float ylo = wave_min_f32(fast ? y : inf), yhi = wave_max_f32(fast ? y : -inf);
+        if (mine && (ylo > 0.0f || yhi < 0.0f)) {
+            const float c1 = box[a] - o, c2 = box[3 + a] - o;  // PtAabb: bmin[3], bmax[3]
+            const float p1 = c1 * ylo, p2 = c1 * yhi, p3 = c2 * ylo, p4 = c2 * yhi;
+            lo = pt_gmax(lo, pt_gmin(pt_gmin(p1, p2), pt_gmin(p3, p4)));
+            hi = pt_gmin(hi, pt_gmax(pt_gmax(p1, p2), pt_gmax(p3, p4)));
+        }
+    };
+    axis(0, rd.x, ox);
+    axis(1, rd.y, oy);
+    axis(2, rd.z, oz);
+    const bool skip = mine && (hi <= 0.0f ||
+                               (lo > 0.0f && hi > 0.0f && __float_as_uint(lo) > __float_as_uint(hi) + PT_ULP_MARGIN));
+    return __ballot(skip);
+}
 
 __device__ __forceinline__ void store_ray(PtRay *r, const pt_f3 &ro, const pt_f3 &rd, const pt_f3 &thr, uint32_t rng,
                                           uint32_t sid, uint32_t aux, const uint4 &q3) {
@@ -583,9 +658,16 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             pixel_of(L, pl, x, y);
             uint32_t rg;
             pt_f3 o, d;
-            camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), L.width, L.height, L.aspect, L.fov, rg, o, d);
+            // (fov through an empty asm: normalize's fov * fov, hoisted out of
+            // the persistent loop, held a register there and spilled)
+            float fov = L.fov;
+            __asm__ volatile("" : "+v"(fov));
+            camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), L.width, L.height, L.aspect, fov, rg, o, d);
             st.add(PT_ST_SAMPLES);
-            const uint4 m = MapBounds<Map>::template mask<ST>(L, o, d, st);
+            // the boxes no camera ray of the window can hit (every lane of a
+            // full window is here, as the skip's wave reductions need)
+            const uint64_t skip = wcnt == 64u ? primary_box_skip(L, o, d) : 0ull;
+            const uint4 m = MapBounds<Map>::template mask_skip<ST>(L, o, d, skip, st);
             s0 = make_float4(o.x, o.y, o.z, d.x);
             s1 = make_float4(d.y, d.z, 1.0f, 1.0f);
             s2 = make_float4(1.0f, __uint_as_float(rg), __uint_as_float(i), __uint_as_float(i));  // (aux: its slot)

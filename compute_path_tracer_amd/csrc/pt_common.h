@@ -93,6 +93,31 @@ __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
 __device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
     return uint64_t(wave_or_u32(uint32_t(v))) | (uint64_t(wave_or_u32(uint32_t(v >> 32))) << 32);
 }
+// min / max of v over the 64 lanes (every lane active; a lane that must not
+// count passes the identity, +inf / -inf), wave-uniform: the same scan as
+// fused v_min / v_max_f32_dpp.  A lane without a source lane (row edge,
+// bound_ctrl off) is not written and keeps its value.  Two wait states before
+// each step (a VALU write read by the next DPP), which the compiler cannot
+// see inside the asm.  (The builtin form, update_dpp + min with the identity
+// shifted in, compiled to three instructions per step: the first pass's
+// kernel 25.5 vs 24.9 ms per launch, profiles/r05i_*.)
+#define PT_WRED_ASM(op, v)                                                                          \
+    __asm__ volatile("s_nop 1\n\t" op "_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"     \
+                     "s_nop 1\n\t" op "_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"     \
+                     "s_nop 1\n\t" op "_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"     \
+                     "s_nop 1\n\t" op "_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"     \
+                     "s_nop 1\n\t" op "_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"  \
+                     "s_nop 1\n\t" op "_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"  \
+                     "s_nop 1"                                                                      \
+                     : "+v"(v))
+__device__ __forceinline__ float wave_min_f32(float v) {
+    PT_WRED_ASM("v_min_f32", v);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_max_f32(float v) {
+    PT_WRED_ASM("v_max_f32", v);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 
 __device__ __forceinline__ int lane_rank(uint64_t m) {  // set bits of m below this lane
     return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));

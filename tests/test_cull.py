@@ -395,3 +395,16 @@ def test_wave_fallback_is_per_kernel():
     if int(spilled.get("pt_bin_shade_t_jit", 0)) > 16:
         want.add("PT_SW_N=7")
     assert lowered == want, (lowered, spilled)
+
+
+@pytest.mark.parametrize("scene", ["c3", "wide"])
+def test_primary_box_skip_guards(scene, tmp_path):
+    """bounds()' fast path takes the first pass's box-skip hint (DESIGN.md
+    3.20) as one guard per box below 64 -- primary_box_skip covers at most 64
+    boxes, and a shift by 64 or more would be undefined (a 120-box scene's
+    kernels faulted with such guards) -- and none above."""
+    src, _ = _baked(scene, tmp_path)
+    prog = scenes.SCENES[scene]().compile(CompData())
+    shifts = [int(k) for k in re.findall(r"if \(!\(\(skip >> (\d+)\) & 1ull\)\)", src)]
+    assert shifts == list(range(min(64, prog.n_aabb)))
+    assert "mask_skip<ST>(L, ro, rd, 0ull, st)" in src  # the shade pass passes no hint
