@@ -110,6 +110,20 @@ def test_wave_kernel_schedule_invariance(gpu, shade_batch, kernel):
     assert exact == 1.0, (shade_batch, rms)
 
 
+@pytest.mark.parametrize("kernel", ["binned_jit", "binned_tier"])
+@pytest.mark.parametrize("fov", [0.02, 1.0, 5.0])
+def test_first_pass_box_skip_edges(gpu, kernel, fov):
+    """The first pass's wave-level box skip at its edges:
+    72x40 puts windows across the image centre (uv = 0, so a window's rd.x
+    or rd.y changes sign and that axis gives no bound), and a narrow and a
+    wide field of view (fov is rd.z before normalising: at 0.02 a window's
+    rays are nearly parallel to the image plane's axes, at 5 nearly along
+    z).  Bit-exact against the oracle on C3's 24 boxes."""
+    gpu_img, ref = _render_pair(scenes.c3_graph32(), 72, 40, 2, 3, fov=fov, kernel=kernel)
+    rms, exact = _report(gpu_img, ref)
+    assert exact == 1.0 and rms == 0.0, (rms, exact)
+
+
 @pytest.mark.parametrize("kernel", ["jit", "binned_jit"])
 def test_long_dispatch_chunks(gpu, kernel):
     """spp > 64 is split into several launches that continue frame/last_clear."""
