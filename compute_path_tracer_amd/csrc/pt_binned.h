@@ -87,6 +87,7 @@ struct PtPass {
     const uint32_t *n_src;  // rin slots (bounds / scatter), null: n_src_const
     float4 *color;          // [frames][n_pix] sample colours
     float4 *hitn;           // trace -> shade: check[] bits 64..127 of a hit (.zw; scenes with > 64 entries)
+    unsigned long long *btab;  // [PT_BINS] check[] set + 1 per bin (0: free), null: hashed bins (bin_of)
     uint32_t n_src_const;
     int32_t bounce;         // segment index of this pass (path_trace's loop counter i)
     int32_t n_pix;          // local pixel slots: n_tiles * 64
@@ -103,10 +104,42 @@ struct PtPass {
 
 namespace pt {
 
-__device__ __forceinline__ uint32_t bin_of(const uint4 &m) {
-    if ((m.y | m.z | m.w) == 0u && m.x < uint32_t(PT_BINS)) return m.x;  // small scenes: the exact set
+__device__ __forceinline__ uint32_t bin_hash(const uint4 &m) {
     const uint32_t h = (m.x * 0x9E3779B1u) ^ (m.y * 0x85EBCA77u) ^ (m.z * 0xC2B2AE3Du) ^ (m.w * 0x27D4EB2Fu);
     return (h ^ (h >> 15)) * 0x2C1B3C6Du >> (32 - PT_BIN_BITS);
+}
+
+// The bin of a check[] set.  Scenes with at most PT_BIN_BITS entries: the set
+// itself.  Wider scenes: a hash would put two sets in one bin now and then,
+// and a trace window of that bin then evaluates the union of both sets'
+// shapes (C3: ~4900 distinct sets seen; a 64-ray window of a hashed bin admits
+// ~2.6 boxes where its own set has ~1.8).  So with P.btab
+// (scenes of 13..64 entries) the bin is the set's slot in a table of sets,
+// open addressing from the hash: the first lane to see a set claims a free
+// slot with a CAS, every later one finds it.  Only the schedule depends on
+// the table (the host clears it per dispatch); a set that finds no slot
+// within PT_BIN_PROBES shares its hash bin as before.
+#ifndef PT_BIN_PROBES
+#define PT_BIN_PROBES 8
+#endif
+__device__ __forceinline__ uint32_t bin_of(const PtPass &P, const uint4 &m) {
+    if (!P.btab) {
+        if ((m.y | m.z | m.w) == 0u && m.x < uint32_t(PT_BINS)) return m.x;  // small scenes: the exact set
+        return bin_hash(m);
+    }
+    const uint32_t h = bin_hash(m);
+    const unsigned long long e = ((unsigned long long)m.y << 32 | m.x) + 1ull;  // (0: a free slot)
+    if (e == 0ull) return h;
+    uint32_t s = h;
+    for (int k = 0; k < PT_BIN_PROBES; ++k) {
+        // (a plain load: a slot only ever goes from 0 to its set, so a stale
+        // 0 just sends the lane to the CAS, which returns the slot's set)
+        unsigned long long v = P.btab[s];
+        if (v == 0ull) v = atomicCAS(P.btab + s, 0ull, e);
+        if (v == 0ull || v == e) return s;
+        s = (s + 1u) & uint32_t(PT_BINS - 1);
+    }
+    return h;
 }
 
 // bounds() of one ray, one thread: every box's slab test (scalar box loads).
@@ -316,7 +349,7 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
         P.color[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the path's radiance (ret) starts at 0
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         if (!P.gen_order) {
-            const uint32_t b = bin_of(m);
+            const uint32_t b = bin_of(P, m);
             P.key[i] = b;
             atomicAdd(&lh[b], 1u);
         }
@@ -438,7 +471,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
         store_ray(P.rout + i, ro, rd, thr, rng, sid, i, make_uint4(m.x, m.y, 0u, 0u));
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
-        const uint32_t k = bin_of(m);
+        const uint32_t k = bin_of(P, m);
         P.key[i] = k;
         atomicAdd(&lh[k], 1u);
     };

@@ -112,6 +112,8 @@ struct pt_ctx {
     hipStream_t xstream[kMaxLanes] = {};   // lanes 1.. streams (created on first use; lane 0 = stream)
     hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {};
     int bin_lanes = 2;                     // pt_set_option "bin_lanes" (2: +6 % over 1; 3-4 equal or worse)
+    int bin_table = 1;                     // pt_set_option "bin_table": bins from the table of check[] sets
+    unsigned long long *d_btab = nullptr;  // that table, [PT_BINS] (pt_binned.h bin_of), shared by the lanes
     int shade_taps = 1;                    // pt_set_option "shade_taps": normal taps in the shade pass
     int gen_trace_used = 0;                // the last timed dispatch's first pass made its own camera rays
     int cu_count = 0;
@@ -694,6 +696,8 @@ static void free_bin(pt_ctx *c) {
     }
     (void)hipFree(c->d_color);
     c->d_color = nullptr;
+    (void)hipFree(c->d_btab);
+    c->d_btab = nullptr;
     c->n_lanes = 0;
     c->bin_cap = c->ctrl_words = 0;
 }
@@ -708,7 +712,8 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
     samples = std::max(samples, c->bin_cap);
     lanes = std::max(lanes, c->n_lanes);
     free_bin(c);
-    bool ok = hipMalloc(&c->d_color, size_t(lanes) * samples * sizeof(float4)) == hipSuccess;
+    bool ok = hipMalloc(&c->d_color, size_t(lanes) * samples * sizeof(float4)) == hipSuccess &&
+              hipMalloc(&c->d_btab, PT_BINS * sizeof(unsigned long long)) == hipSuccess;
     for (int i = 0; ok && i < lanes; ++i) {
         pt_ctx::BinLane &l = c->lane[i];
         ok = hipMalloc(&l.ray[0], samples * sizeof(PtRay)) == hipSuccess &&
@@ -859,6 +864,13 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             fl[i] = fr / uint32_t(nl) + (uint32_t(i) < fr % uint32_t(nl) ? 1u : 0u);
             fo[i] = i == 0 ? 0u : fo[i - 1] + fl[i - 1];
         }
+        // the table of check[] sets starts empty per chunk (bin_of: only
+        // scenes whose sets do not fit the bin index use it)
+        unsigned long long *btab = nullptr;
+        if (c->bin_table && c->n_check > uint32_t(PT_BIN_BITS) && c->n_check <= 64) {
+            btab = c->d_btab;
+            HIPCHK(c, hipMemsetAsync(btab, 0, PT_BINS * sizeof(unsigned long long), c->stream));
+        }
         PtPass P[pt_ctx::kMaxLanes];
         for (int i = 0; i < nl; ++i) {
             const pt_ctx::BinLane &l = c->lane[i];
@@ -884,6 +896,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             p.n_pix = int32_t(n_pix);
             p.frames = int32_t(fl[i]);
             p.wide = c->n_check > 64 ? 1 : 0;
+            p.btab = btab;
             p.run_max = run_max;
             p.refill_min = refill_min;
         }
@@ -1269,6 +1282,11 @@ int pt_set_option(pt_ctx *c, const char *key, int value) {
         c->bin_lanes = value;
         return PT_OK;
     }
+    if (!std::strcmp(key, "bin_table")) {
+        if (value < 0 || value > 1) return fail(c, PT_ERR_INVALID, "bin_table must be 0 or 1");
+        c->bin_table = value;
+        return PT_OK;
+    }
     if (!std::strcmp(key, "shade_taps")) {
         if (value < 0 || value > 1) return fail(c, PT_ERR_INVALID, "shade_taps must be 0 or 1");
         c->shade_taps = value;
@@ -1315,6 +1333,7 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "shade_ms")) HIPCHK(c, event_log_ms(c->slog, value));  // summed over the shade passes
     else if (!std::strcmp(key, "bin_bytes")) *value = double(c->bin_cap) * double(c->n_lanes) * double(bin_bytes_per_sample(c));
     else if (!std::strcmp(key, "bin_lanes")) *value = double(c->bin_lanes);
+    else if (!std::strcmp(key, "bin_table")) *value = double(c->bin_table);
     else if (!std::strcmp(key, "shade_taps")) *value = c->shade_taps ? 1.0 : 0.0;
     else if (!std::strcmp(key, "jit_cache")) {
         // where the scene kernel in use came from: 1 the shipped on-disk cache

@@ -237,7 +237,9 @@ int pt_display(pt_ctx *ctx, int format, void *out, size_t bytes);
  * the context's first binned dispatch), "bin_lanes"
  * (binned kernel: 1..4 pipelines, each on its own stream, over which a
  * chunk's frames are split, so one's memory-bound passes overlap another's
- * trace pass), "jit" (1:
+ * trace pass), "bin_table" (binned kernel, scenes with 13..64 check[]
+ * entries: 1, the default, bins each set in a slot of its own from a table
+ * of the sets seen; 0: hashed bins, which two sets share now and then), "jit" (1:
  * per-scene hipRTC build of the state-machine kernels, compiled at
  * pt_set_data when the topology or an identity flag changed -- the analogue
  * of remake_pipeline; 0: op-list interpreter), "jit_bake" (0: node values
@@ -251,7 +253,7 @@ int pt_set_option(pt_ctx *ctx, const char *key, int value);
  * "jit_seconds" (last hipRTC compile time), "jit_tier_active" /
  * "jit_tier_seconds" (values-baked build in use / its compile time),
  * "kernel", "shade_batch",
- * "bin_samples", "bin_lanes", "bin_bytes" (device memory held by the binned
+ * "bin_samples", "bin_lanes", "bin_table", "bin_bytes" (device memory held by the binned
  * pipeline), "bin_chunks" (chunks of the last binned dispatch), "bin_fallback"
  * (1: the chunk size came from the free memory), "trace_ms" / "trace_launches" (device time and count of the last
  * dispatch's binned trace passes, HIP events on each pipeline's stream),

@@ -39,10 +39,11 @@ def _tier_up(pt, opts):
 
 
 def _render_pair(ed, w, h, spp, bounces, debug=0, frame=1, last_clear=1, fov=1.0, aspect=None, kernel="jit",
-                 shade_batch=None, bin_samples=None, bin_lanes=None):
+                 shade_batch=None, bin_samples=None, bin_lanes=None, extra=None):
     prog = ed.compile(CompData())
     st = N.Settings(debug=debug, bounces=bounces, scale=1.0, fov=fov, aabb=0)
     opts = dict(KERNELS[kernel])
+    opts.update(extra or {})
     if shade_batch:
         opts["shade_batch"] = shade_batch
     if bin_samples:
@@ -151,6 +152,20 @@ def test_binned_lanes(gpu, bin_lanes, spp, bin_samples):
                                 bin_lanes=bin_lanes)
     rms, exact = _report(gpu_img, ref)
     assert exact == 1.0, rms
+
+
+@pytest.mark.parametrize("kernel", ["binned", "binned_jit", "binned_tier"])
+@pytest.mark.parametrize("bin_table", [0, 1])
+@pytest.mark.parametrize("name,spp,bin_lanes", [("c3", 4, 2), ("c3", 3, 3), ("cull", 3, 1), ("c3_noaabb", 2, 2)])
+def test_bin_table_schedule_only(gpu, kernel, bin_table, name, spp, bin_lanes):
+    """Bins from the table of check[] sets (pt_binned.h bin_of, DESIGN.md
+    3.21) or from the hash: the schedule changes, the image does not.  C3
+    (24 boxes) and `cull` use the table, with one to three pipelines sharing
+    it; C3 without boxes has one set."""
+    gpu_img, ref = _render_pair(scenes.SCENES[name](), 96, 54, spp, 8, kernel=kernel, bin_lanes=bin_lanes,
+                                extra={"bin_table": bin_table})
+    rms, exact = _report(gpu_img, ref)
+    assert exact == 1.0 and rms == 0.0, (rms, exact)
 
 
 @pytest.mark.parametrize("kernel", ["jit", "binned_jit"])
