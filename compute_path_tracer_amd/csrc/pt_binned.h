@@ -87,7 +87,7 @@ struct PtPass {
     const uint32_t *n_src;  // rin slots (bounds / scatter), null: n_src_const
     float4 *color;          // [frames][n_pix] sample colours
     float4 *hitn;           // trace -> shade: check[] bits 64..127 of a hit (.zw; scenes with > 64 entries)
-    unsigned long long *btab;  // [PT_BINS] check[] set + 1 per bin (0: free), null: hashed bins (bin_of)
+    unsigned long long *btab;  // [PT_BINS] check[] set + 1 per bin (0: free), null: hashed bins (bin_resolve)
     uint32_t n_src_const;
     int32_t bounce;         // segment index of this pass (path_trace's loop counter i)
     int32_t n_pix;          // local pixel slots: n_tiles * 64
@@ -122,24 +122,47 @@ __device__ __forceinline__ uint32_t bin_hash(const uint4 &m) {
 #ifndef PT_BIN_PROBES
 #define PT_BIN_PROBES 8
 #endif
-__device__ __forceinline__ uint32_t bin_of(const PtPass &P, const uint4 &m) {
-    if (!P.btab) {
-        if ((m.y | m.z | m.w) == 0u && m.x < uint32_t(PT_BINS)) return m.x;  // small scenes: the exact set
-        return bin_hash(m);
-    }
-    const uint32_t h = bin_hash(m);
-    const unsigned long long e = ((unsigned long long)m.y << 32 | m.x) + 1ull;  // (0: a free slot)
-    if (e == 0ull) return h;
-    uint32_t s = h;
-    for (int k = 0; k < PT_BIN_PROBES; ++k) {
+// In two steps, so a pass can issue the first probe's load before it stores
+// the ray and compare after: vmcnt counts stores as well as loads (gfx9), so
+// a load issued behind the ray's stores would wait for them too (the shade
+// pass: +10 points of its wave time at s_waitcnt, 3.21).
+struct BinProbe {
+    uint32_t h;              // the hash bin: the first slot
+    unsigned long long e;    // the set + 1 (0: not in the table)
+    unsigned long long v;    // the first slot's content
+};
+__device__ __forceinline__ BinProbe bin_probe(const PtPass &P, const uint4 &m) {
+    BinProbe b;
+    b.h = bin_hash(m);
+    b.e = 0ull;
+    b.v = 0ull;
+    if (P.btab) {
+        b.e = ((unsigned long long)m.y << 32 | m.x) + 1ull;  // (0: a free slot)
         // (a plain load: a slot only ever goes from 0 to its set, so a stale
         // 0 just sends the lane to the CAS, which returns the slot's set)
-        unsigned long long v = P.btab[s];
-        if (v == 0ull) v = atomicCAS(P.btab + s, 0ull, e);
-        if (v == 0ull || v == e) return s;
-        s = (s + 1u) & uint32_t(PT_BINS - 1);
+        if (b.e != 0ull) b.v = P.btab[b.h];
     }
-    return h;
+    return b;
+}
+__device__ __forceinline__ uint32_t bin_resolve(const PtPass &P, const uint4 &m, BinProbe b) {
+    if (!P.btab) {
+        if ((m.y | m.z | m.w) == 0u && m.x < uint32_t(PT_BINS)) return m.x;  // small scenes: the exact set
+        return b.h;
+    }
+    // (the set already in its hash slot, nearly every lane after a pass's
+    // first waves, returns before the claim below, so the claim's wait for
+    // its CAS -- a vmcnt(0), the ray's stores included -- runs only in waves
+    // with a lane that claims or probes on)
+    if (b.e == 0ull || b.v == b.e) return b.h;
+    uint32_t s = b.h;
+    unsigned long long v = b.v;
+    for (int k = 0;;) {
+        if (v == 0ull) v = atomicCAS(P.btab + s, 0ull, b.e);
+        if (v == 0ull || v == b.e) return s;
+        if (++k == PT_BIN_PROBES) return b.h;
+        s = (s + 1u) & uint32_t(PT_BINS - 1);
+        v = P.btab[s];
+    }
 }
 
 // bounds() of one ray, one thread: every box's slab test (scalar box loads).
@@ -345,11 +368,12 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
         camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), L.width, L.height, L.aspect, L.fov, rng, ro, rd);
         st.add(PT_ST_SAMPLES);
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
+        const BinProbe bp = P.gen_order ? BinProbe{0u, 0ull, 0ull} : bin_probe(P, m);  // (before the stores)
         store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, rng, i, i, make_uint4(m.x, m.y, 0u, 0u));
         P.color[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the path's radiance (ret) starts at 0
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         if (!P.gen_order) {
-            const uint32_t b = bin_of(P, m);
+            const uint32_t b = bin_resolve(P, m, bp);
             P.key[i] = b;
             atomicAdd(&lh[b], 1u);
         }
@@ -469,9 +493,10 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             return;
         }
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
+        const BinProbe bp = bin_probe(P, m);  // (before the stores: bin_probe)
         store_ray(P.rout + i, ro, rd, thr, rng, sid, i, make_uint4(m.x, m.y, 0u, 0u));
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
-        const uint32_t k = bin_of(P, m);
+        const uint32_t k = bin_resolve(P, m, bp);
         P.key[i] = k;
         atomicAdd(&lh[k], 1u);
     };
@@ -484,7 +509,11 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             if (q2.w == PT_AUX_MISS) P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
             else shade_one(i, q0, q1, q2, q3, make_uint2(0u, 0u), q3);
         } else {
-            const uint4 hq = P.hq[i];
+            uint4 hq = P.hq[i];
+            // (the whole quad in one load before the miss test: left alone,
+            // the compiler loads .yz, tests, then loads .xw inside the
+            // branch -- a second round trip before the ray's gather)
+            __asm__ volatile("" : "+v"(hq.x), "+v"(hq.y), "+v"(hq.z), "+v"(hq.w));
             if (hq.y == PT_AUX_MISS) {
                 P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
                 continue;

@@ -113,7 +113,7 @@ struct pt_ctx {
     hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {};
     int bin_lanes = 2;                     // pt_set_option "bin_lanes" (2: +6 % over 1; 3-4 equal or worse)
     int bin_table = 1;                     // pt_set_option "bin_table": bins from the table of check[] sets
-    unsigned long long *d_btab = nullptr;  // that table, [PT_BINS] (pt_binned.h bin_of), shared by the lanes
+    unsigned long long *d_btab = nullptr;  // that table, [PT_BINS] (pt_binned.h bin_probe / bin_resolve), shared by the lanes
     int shade_taps = 1;                    // pt_set_option "shade_taps": normal taps in the shade pass
     int gen_trace_used = 0;                // the last timed dispatch's first pass made its own camera rays
     int cu_count = 0;
@@ -864,7 +864,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             fl[i] = fr / uint32_t(nl) + (uint32_t(i) < fr % uint32_t(nl) ? 1u : 0u);
             fo[i] = i == 0 ? 0u : fo[i - 1] + fl[i - 1];
         }
-        // the table of check[] sets starts empty per chunk (bin_of: only
+        // the table of check[] sets starts empty per chunk (bin_resolve: only
         // scenes whose sets do not fit the bin index use it)
         unsigned long long *btab = nullptr;
         if (c->bin_table && c->n_check > uint32_t(PT_BIN_BITS) && c->n_check <= 64) {
