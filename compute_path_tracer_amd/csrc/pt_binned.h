@@ -100,6 +100,9 @@ struct PtPass {
     int32_t gen_trace;      // first pass without a gen pass (scene kernels, generation order): the trace
                             // pass makes each window's camera rays and bounds() itself, a miss zeroes its
                             // colour slot, and the shade pass stores (not adds) the first segment's emission
+    int32_t gen_norec;      // gen_trace, check[] of <= 32 entries: the first pass writes no ray records -- its
+                            // hit quads carry the ray's check[] bits in .w (the slot is the position) -- and
+                            // shade pass 0 makes each traced camera ray again (camera_ray: the same bits)
 };
 
 namespace pt {
@@ -333,11 +336,14 @@ __device__ __forceinline__ void hist_flush(const uint32_t *lh, uint32_t *hist) {
         if (lh[b] != 0u) atomicAdd(&hist[b], lh[b]);
 }
 // local pixel slot -> image coordinates (cyclic tile ownership, as pt_wave.h)
-__device__ __forceinline__ void pixel_of(const PtLaunch &L, uint32_t pl, int &x, int &y) {
+__device__ __forceinline__ void pixel_of(int rank, int nranks, int tiles_x, uint32_t pl, int &x, int &y) {
     const int k = int(pl >> 6), p = int(pl & 63u);
-    const int g = L.rank + k * L.nranks;
-    x = (g % L.tiles_x) * PT_TILE + (p & 7);
-    y = (g / L.tiles_x) * PT_TILE + (p >> 3);
+    const int g = rank + k * nranks;
+    x = (g % tiles_x) * PT_TILE + (p & 7);
+    y = (g / tiles_x) * PT_TILE + (p >> 3);
+}
+__device__ __forceinline__ void pixel_of(const PtLaunch &L, uint32_t pl, int &x, int &y) {
+    pixel_of(L.rank, L.nranks, L.tiles_x, pl, x, y);
 }
 
 // gen: camera ray + bounds() of every (frame, pixel) of the chunk
@@ -518,8 +524,38 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                 P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
                 continue;
             }
-            const PtRay *r = P.rin + hq.w;
-            const uint4 q0 = r->q[0], q1 = r->q[1], q2 = r->q[2], q3 = r->q[3];
+            uint4 q0, q1, q2, q3;
+            if (P.gen_norec) {
+                // shade pass 0 without ray records: the traced camera ray of
+                // sample i (its slot is its position) made again, as the first
+                // pass made it (bin_trace_body stage), check[] bits from the quad
+                // (the launch's scalars through an empty asm: left alone, the
+                // compiler hoists what depends only on them -- the integer
+                // divisions' reciprocals, float(height), fov * fov -- out of the
+                // loop into registers held across the whole body, where they
+                // spill)
+                uint32_t npix = uint32_t(P.n_pix);
+                int rk = L.rank, nr = L.nranks, tx = L.tiles_x, cw = L.width, chh = L.height;
+                float ca = L.aspect, cf = L.fov;
+                __asm__ volatile("" : "+s"(npix), "+s"(rk), "+s"(nr), "+s"(tx), "+s"(cw), "+s"(chh), "+s"(ca),
+                                 "+s"(cf));
+                const uint32_t f = i / npix, pl = i - f * npix;
+                int x, y;
+                pixel_of(rk, nr, tx, pl, x, y);
+                uint32_t rg;
+                pt_f3 o, d;
+                camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), cw, chh, ca, cf, rg, o, d);
+                q0 = make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(d.x));
+                q1 = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), __float_as_uint(1.0f), __float_as_uint(1.0f));
+                q2 = make_uint4(__float_as_uint(1.0f), rg, i, i);
+                q3 = make_uint4(hq.w, 0u, 0u, 0u);
+            } else {
+                const PtRay *r = P.rin + hq.w;
+                q0 = r->q[0];
+                q1 = r->q[1];
+                q2 = r->q[2];
+                q3 = r->q[3];
+            }
             uint2 hi = make_uint2(0u, 0u);
             if (wide_of<Map>(P)) {
                 const float4 nd = P.hitn[i];
@@ -776,7 +812,8 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                     store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
                               make_uint4(__float_as_uint(dv0), __float_as_uint(dv1), __float_as_uint(dv2), 0u));
                 } else {  // hit quad: t, material, tap bound, slot (bin_shade_body)
-                    P.hq[pos] = make_uint4(__float_as_uint(t), uint32_t(mat), __float_as_uint(dv0), slot);
+                    P.hq[pos] = make_uint4(__float_as_uint(t), uint32_t(mat), __float_as_uint(dv0),
+                                           GEN && P.gen_norec ? uint32_t(ck.lo) : slot);
                     if (wide_of<Map>(P))
                         P.hitn[pos] = make_float4(0.0f, 0.0f, __uint_as_float(uint32_t(ck.hi)),
                                                   __uint_as_float(uint32_t(ck.hi >> 32)));
@@ -809,8 +846,10 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             if (wide_of<Map>(P)) W[4][lane] = make_uint4(sh.x, sh.y, 0u, 0u);
         if constexpr (GEN) {
             // the window's camera rays at their slots for the shade pass: 64
-            // lanes, 64 contiguous records (whole lines)
-            if (in_win) {
+            // lanes, 64 contiguous records (whole lines) -- unless shade pass
+            // 0 makes them again (gen_norec: 64 B per sample neither written
+            // here nor gathered there)
+            if (in_win && !P.gen_norec) {
                 uint4 *r = reinterpret_cast<uint4 *>(P.rin + wbase + uint32_t(lane));
                 r[0] = make_uint4(__float_as_uint(s0.x), __float_as_uint(s0.y), __float_as_uint(s0.z),
                                   __float_as_uint(s0.w));

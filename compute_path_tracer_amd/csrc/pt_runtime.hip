@@ -925,6 +925,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         for (int i = 0; i < nl; ++i) {
             if (P[i].gen_order && jit && taps_shade && !stats && jm->trace_g) {
                 P[i].gen_trace = 1;
+                P[i].gen_norec = c->n_check <= 32 ? 1 : 0;  // (the check[] bits ride in the hit quad)
                 c->gen_trace_used = 1;
             } else if (jit) {
                 void *args[] = {&P[i]};
@@ -964,7 +965,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
                 PtPass &p = P[i];
                 if (k > 0 && (rc = shade(i, k - 1)) != PT_OK) return rc;
                 const bool gt = k == 0 && p.gen_trace;
-                if (k > 0) p.gen_trace = 0;  // (shade pass 0 above still had it)
+                if (k > 0) p.gen_trace = p.gen_norec = 0;  // (shade pass 0 above still had them)
                 p.bounce = k;
                 p.rin = l.ray[k & 1];
                 p.rout = l.ray[(k + 1) & 1];
