@@ -113,7 +113,7 @@ def algorithmic_flops(st: dict) -> float:
     return float(f)
 
 
-def pipeline_bytes(st: dict, pixels: float, gen_trace: bool = False) -> dict:
+def pipeline_bytes(st: dict, pixels: float, gen_trace: bool = False, gen_norec: bool = False) -> dict:
     """Algorithmic HBM bytes of one dispatch of the binned pipeline
     (pt_binned.h), from the instrumented run's counters: S samples, G
     segments (rays entering a trace pass), H shaded hits.  Misses G - H end
@@ -132,7 +132,11 @@ def pipeline_bytes(st: dict, pixels: float, gen_trace: bool = False) -> dict:
       gathered by slot) and writes the next ray + key (64 + 4 B) or a NONE
       key (4 B);
     - fold reads each frame's colour (16 B) and reads + writes the texel
-      (32 B per pixel).
+      (32 B per pixel);
+    - gen_norec (gen_trace with <= 32 check[] entries, the bench scene): the
+      first pass stores no rays, and shade pass 0 makes its hits' camera rays
+      again instead of gathering them (64 B less per sample in the trace
+      pass and per first-segment hit, `shaded_first`, in the shade pass).
     Not counted: the colour slot's read-modify-write at emitting hits after
     the first (32 B each; no counter separates them) and the high mask words
     of scenes with > 64 check[] entries (the bench scene has 24)."""
@@ -142,8 +146,9 @@ def pipeline_bytes(st: dict, pixels: float, gen_trace: bool = False) -> dict:
     traced_in = G - S if gen_trace else G
     parts = {"gen": 0.0 if gen_trace else 84.0 * S,
              "scatter": 8.0 * cont,
-             "trace": 68.0 * traced_in + 16.0 * G + (64.0 * S if gen_trace else 0.0),
-             "shade": 16.0 * G + 64.0 * H + 68.0 * cont + 4.0 * (ended + miss),
+             "trace": 68.0 * traced_in + 16.0 * G + (64.0 * S if gen_trace and not gen_norec else 0.0),
+             "shade": 16.0 * G + 64.0 * (H - (float(st["shaded_first"]) if gen_norec else 0.0)) + 68.0 * cont
+             + 4.0 * (ended + miss),
              "fold": 16.0 * S + 32.0 * pixels}
     if gen_trace:
         parts["colour0"] = 16.0 * S
@@ -810,7 +815,8 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
     image_bytes = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per dispatch
     jit = bool(pt.get_option("jit_active"))
     gen_trace = bool(pt.get_option("gen_trace"))
-    pipe = pipeline_bytes(st, rank_pixels, gen_trace=gen_trace)
+    gen_norec = bool(pt.get_option("gen_norec"))
+    pipe = pipeline_bytes(st, rank_pixels, gen_trace=gen_trace, gen_norec=gen_norec)
     shade_taps = bool(pt.get_option("shade_taps")) and jit
     n_aabb = prog.n_aabb
     shade = None

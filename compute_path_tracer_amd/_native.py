@@ -35,10 +35,11 @@ STAT_NAMES = (
     "wave_maps", "wave_shapes", "wave_iters", "lane_idle", "idle_shade", "idle_free",
     # wavefront kernel, wave-clock cycles (s_memtime) per phase, summed over waves
     "cyc_refill", "cyc_bounds", "cyc_map", "cyc_shade", "cyc_total",
-    "culled", "wave_evals", "bounds_waves", "bounds_exact", "reserved31",
+    "culled", "wave_evals", "bounds_waves", "bounds_exact",
+    "shaded_first",  # binned pipeline: hits shaded in shade pass 0
 )
 
-PT_ST_COUNT = STAT_NAMES.index("reserved31")  # device counters (pt_device.h PT_ST_COUNT)
+PT_ST_COUNT = len(STAT_NAMES)  # device counters (pt_device.h PT_ST_COUNT)
 
 SYMBOLS = (
     "pt_compile_scene", "pt_create", "pt_resize_clear", "pt_set_program", "pt_set_data", "pt_set_tiles",

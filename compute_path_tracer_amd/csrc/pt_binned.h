@@ -477,6 +477,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             stt.add(PT_ST_NORMAL_MAPS, 6);
         }
         const bool done = shade_lane<ST>(mats, L.bounces, mat, dv0, dv1, dv2, 0, rng, ro, rd, thr, ret, seg, st);
+        if (P.bounce == 0) st.add(PT_ST_SHADED_FIRST);
         // ret += emission * throughput (test_compute.glsl:148) on the colour
         // slot: 0 + e, added to the slot, equals the slot plus e (a slot
         // never holds -0), and a zero e changes no slot, so only emitting

@@ -98,6 +98,7 @@ enum {
     PT_ST_WAVE_EVALS,   // wave-level shape evaluations that ran (WAVE_SHAPES minus whole-wave culls)
     PT_ST_BOUNDS_WAVES, // waves that ran bounds()' fast slab tests (first active lane counts)
     PT_ST_BOUNDS_EXACT, // of those, waves with an undecided lane, which redid every box exactly
+    PT_ST_SHADED_FIRST, // hits shaded in the binned pipeline's shade pass 0 (the first segment's hits)
     PT_ST_COUNT
 };
 

@@ -116,6 +116,7 @@ struct pt_ctx {
     unsigned long long *d_btab = nullptr;  // that table, [PT_BINS] (pt_binned.h bin_probe / bin_resolve), shared by the lanes
     int shade_taps = 1;                    // pt_set_option "shade_taps": normal taps in the shade pass
     int gen_trace_used = 0;                // the last timed dispatch's first pass made its own camera rays
+    int gen_norec_used = 0;                // ... and stored no ray records (shade pass 0 made them again)
     int cu_count = 0;
     bool fast_bounds = false;  // every box coordinate inside the reciprocal-division guard
     float bound_k = 0.0f;      // pt_bound_k of the uploaded scene (NaN: no map() bound)
@@ -921,12 +922,13 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         // no gen pass: the first trace pass makes its windows' camera rays
         // itself (scene kernels, generation order: +2.8 %); otherwise the
         // scene's gen kernel (straight-line bounds(): +1.4 % over the AOT one)
-        if (!stats) c->gen_trace_used = 0;
+        if (!stats) c->gen_trace_used = c->gen_norec_used = 0;
         for (int i = 0; i < nl; ++i) {
             if (P[i].gen_order && jit && taps_shade && !stats && jm->trace_g) {
                 P[i].gen_trace = 1;
                 P[i].gen_norec = c->n_check <= 32 ? 1 : 0;  // (the check[] bits ride in the hit quad)
                 c->gen_trace_used = 1;
+                c->gen_norec_used = P[i].gen_norec;
             } else if (jit) {
                 void *args[] = {&P[i]};
                 HIPCHK(c, hipModuleLaunchKernel(stats ? jm->gen_stats : jm->gen, item_grid(size_t(P[i].n_src_const)), 1,
@@ -1342,6 +1344,7 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
         *value = c->jit_tier.module ? c->tier_from : (c->jit_mod.module ? c->jit_from : -1);
     }
     else if (!std::strcmp(key, "gen_trace")) *value = double(c->gen_trace_used);
+    else if (!std::strcmp(key, "gen_norec")) *value = double(c->gen_norec_used);
     else if (!std::strncmp(key, "tap_stat_", 9)) {  // tap_stat_<k>: counter k of the last stats run's shade-pass taps
         const int k = std::atoi(key + 9);
         if (k < 0 || k >= PT_ST_COUNT) return fail(c, PT_ERR_INVALID, "tap_stat index out of range");

@@ -209,7 +209,8 @@ int pt_sync(pt_ctx *ctx);
  * pt_dispatch, in ms; blocks until they finished. */
 int pt_last_dispatch_ms(pt_ctx *ctx, float *ms);
 /* Instrumented re-run of one dispatch (does not touch the image): per-event
- * work counters for algorithmic-flop accounting. */
+ * work counters for algorithmic-flop accounting, in the order
+ * of compute_path_tracer_amd/_native.py STAT_NAMES. */
 #define PT_STAT_COUNT 32
 int pt_dispatch_stats(pt_ctx *ctx, const pt_constants *c, const pt_settings *s, uint32_t spp,
                       uint64_t counters[PT_STAT_COUNT]);
@@ -258,7 +259,9 @@ int pt_set_option(pt_ctx *ctx, const char *key, int value);
  * (1: the chunk size came from the free memory), "trace_ms" / "trace_launches" (device time and count of the last
  * dispatch's binned trace passes, HIP events on each pipeline's stream),
  * "shade_ms" / "shade_launches" (the same for its shade passes), "display_ms"
- * (device time of the last pt_display's kernel). */
+ * (device time of the last pt_display's kernel), "gen_trace" / "gen_norec"
+ * (the last timed binned dispatch's first pass made its own camera rays /
+ * and stored no ray records for shade pass 0). */
 int pt_get_option(pt_ctx *ctx, const char *key, double *value);
 /* Log of the last failed scene-kernel build ("" if none). */
 const char *pt_jit_log(const pt_ctx *ctx);

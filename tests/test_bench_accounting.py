@@ -51,11 +51,18 @@ def test_flop_split_covers_the_pipeline_once(counters, gen_trace):
 
 def test_pipeline_bytes_add_up(counters):
     _, ct, pixels = counters
-    for gen_trace in (True, False):
-        parts = bench.pipeline_bytes(ct, pixels, gen_trace=gen_trace)
+    # (the oracle does not count first-segment hits; a stand-in below the samples)
+    ct = dict(ct, shaded_first=ct["samples"] * 3 // 4)
+    for gen_trace, gen_norec in ((True, False), (False, False), (True, True)):
+        parts = bench.pipeline_bytes(ct, pixels, gen_trace=gen_trace, gen_norec=gen_norec)
         assert parts["total"] == pytest.approx(sum(v for k, v in parts.items() if k not in ("total", "trace_m", "trace_first")))
         assert parts["trace_m"] + parts["trace_first"] == pytest.approx(parts["trace"])
         assert parts["fold"] == 16.0 * ct["samples"] + 32.0 * pixels
+    # no records in the first pass: 64 B per sample (trace) and per first-segment hit (shade) fewer
+    rec = bench.pipeline_bytes(ct, pixels, gen_trace=True)
+    norec = bench.pipeline_bytes(ct, pixels, gen_trace=True, gen_norec=True)
+    assert rec["trace"] - norec["trace"] == pytest.approx(64.0 * ct["samples"])
+    assert rec["shade"] - norec["shade"] == pytest.approx(64.0 * ct["shaded_first"])
 
 
 def test_hw_view_and_cpu_info():

@@ -24,7 +24,7 @@ class _Ctx:
     size = (48, 32)
 
     def get_option(self, key):
-        return {"jit_active": 1, "gen_trace": 1, "shade_taps": 1, "bin_lanes": 2, "jit_tier_active": 1,
+        return {"jit_active": 1, "gen_trace": 1, "gen_norec": 1, "shade_taps": 1, "bin_lanes": 2, "jit_tier_active": 1,
                 "jit_trace_waves": 8, "jit_shade_waves": 8, "jit_cache": 1, "display_ms": 0.01}.get(key, 0.0)
 
     def display(self, srgb8=False):
@@ -123,7 +123,7 @@ def test_profiled_traffic_scaled_to_the_launch(frame, tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
     r = _report(frame)["roofline"]
     _, _, st, _ = frame
-    pipe = bench.pipeline_bytes(st, W * H, gen_trace=True)
+    pipe = bench.pipeline_bytes(st, W * H, gen_trace=True, gen_norec=True)
     assert r["traffic_source"].startswith(os.path.join("profiles", "zz_pmc.json"))  # not the 2-pipeline one
     assert r["traffic"] == 500
     assert r["traffic_algorithmic"] == round(pipe["trace_m"] / 16)  # 18 trace launches less 2 first passes
@@ -156,7 +156,7 @@ def test_march_traffic_halves_the_scattered_quad_writes(frame, tmp_path, monkeyp
     r = json.loads(json.dumps(out))["roofline"]
     assert r["traffic"] == 600 and r["traffic_uncorrected"] == 700  # (1000 + 200, 1400) x 1/2 pipelines
     assert "WRITE_SIZE / 2" in r["traffic_source"]
-    pipe = bench.pipeline_bytes(st, W * H, gen_trace=True)
+    pipe = bench.pipeline_bytes(st, W * H, gen_trace=True, gen_norec=True)
     assert r["traffic_algorithmic"] == round(pipe["trace_m"] / 14)  # 18 launches less 2 x 2 first passes
     assert r["traffic_first_pass"]["algorithmic"] == round(pipe["trace_first"] / 4)
     assert out["config"]["chunks_per_dispatch"] == 2.0
