@@ -168,6 +168,29 @@ def test_bin_table_schedule_only(gpu, kernel, bin_table, name, spp, bin_lanes):
     assert exact == 1.0 and rms == 0.0, (rms, exact)
 
 
+@pytest.mark.parametrize("kernel", ["binned_jit", "binned_tier"])
+@pytest.mark.parametrize("bin_lanes", [1, 2])
+def test_first_pass_without_records(gpu, kernel, bin_lanes):
+    """Whole tiles, so the first pass makes its own camera rays (gen_trace);
+    C3's 24 check[] entries, so it stores no ray records and shade pass 0
+    makes them again, with one and two pipelines:
+    bit-exact against the oracle."""
+    ed = scenes.c3_graph32()
+    prog = ed.compile(CompData())
+    w, h, spp = 64, 48, 6
+    opts = dict(KERNELS[kernel], bin_lanes=bin_lanes)
+    pt = PathTracer(w, h, prog, settings=N.Settings(debug=0, bounces=8, scale=1.0, fov=1.0, aabb=0), options=opts)
+    _tier_up(pt, opts)
+    a = float(np.float32(w) / np.float32(h))
+    pt.dispatch(N.Constants(time=0.0, frame=1, aspect=a, last_clear=1), spp)
+    gpu_img = pt.read_image()
+    assert pt.get_option("gen_trace") == 1.0 and pt.get_option("gen_norec") == 1.0
+    pt.close()
+    ref = O.OracleScene(ed.rows()).render(w, h, O.Constants(0.0, 1, a, 1), O.Settings(0, 8, 1.0, 1.0, 0), spp)
+    rms, exact = _report(gpu_img, ref)
+    assert exact == 1.0 and rms == 0.0, (rms, exact)
+
+
 @pytest.mark.parametrize("kernel", ["jit", "binned_jit"])
 def test_empty_scene_is_black(gpu, kernel):
     gpu_img, ref = _render_pair(scenes.empty(), 40, 24, 2, 4, kernel=kernel)
