@@ -88,6 +88,7 @@ struct PtPass {
     float4 *color;          // [frames][n_pix] sample colours
     float4 *hitn;           // trace -> shade: check[] bits 64..127 of a hit (.zw; scenes with > 64 entries)
     unsigned long long *btab;  // [PT_BINS] check[] set + 1 per bin (0: free), null: hashed bins (bin_resolve)
+    int32_t lanes;          // fold: pipelines that split the chunk's frames (colour regions, bin_fold_body)
     uint32_t n_src_const;
     int32_t bounce;         // segment index of this pass (path_trace's loop counter i)
     int32_t n_pix;          // local pixel slots: n_tiles * 64
@@ -345,6 +346,19 @@ __device__ __forceinline__ void pixel_of(int rank, int nranks, int tiles_x, uint
 __device__ __forceinline__ void pixel_of(const PtLaunch &L, uint32_t pl, int &x, int &y) {
     pixel_of(L.rank, L.nranks, L.tiles_x, pl, x, y);
 }
+// The first pass's position p -> its sample (frame f, local pixel pl), frame
+// fastest: a 64-ray window is one pixel's camera rays of 64 frames (with 64
+// or more frames in the chunk), whose directions differ only by the
+// sub-pixel jitter -- the narrowest bundle for the box skip (3.20) and the
+// most coherent march.  The sample's colour slot stays f * n_pix + pl.
+__device__ __forceinline__ void gen_sample(uint32_t frames, uint32_t p, uint32_t &f, uint32_t &pl) {
+    pl = p / frames;
+    f = p - pl * frames;
+}
+// A sample's colour slot in its pipeline's region: [pixel][frame], so the
+// first pass's position is its sample's slot (gen_sample) and a pixel's
+// frames lie in one run for the fold.
+__device__ __forceinline__ uint32_t colour_slot(uint32_t frames, uint32_t f, uint32_t pl) { return pl * frames + f; }
 
 // gen: camera ray + bounds() of every (frame, pixel) of the chunk
 // (MapBounds<Map>: the generic box loop, or the scene kernels' straight-line
@@ -375,8 +389,9 @@ __device__ __forceinline__ void bin_gen_body(const PtPass &P) {
         st.add(PT_ST_SAMPLES);
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
         const BinProbe bp = P.gen_order ? BinProbe{0u, 0ull, 0ull} : bin_probe(P, m);  // (before the stores)
-        store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, rng, i, i, make_uint4(m.x, m.y, 0u, 0u));
-        P.color[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the path's radiance (ret) starts at 0
+        const uint32_t sid = colour_slot(uint32_t(P.frames), f, pl);
+        store_ray(P.rin + i, ro, rd, pt_f3{1.0f, 1.0f, 1.0f}, rng, sid, i, make_uint4(m.x, m.y, 0u, 0u));
+        P.color[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the path's radiance (ret) starts at 0
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         if (!P.gen_order) {
             const uint32_t b = bin_resolve(P, m, bp);
@@ -535,12 +550,13 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                 // divisions' reciprocals, float(height), fov * fov -- out of the
                 // loop into registers held across the whole body, where they
                 // spill)
-                uint32_t npix = uint32_t(P.n_pix);
+                uint32_t npix = uint32_t(P.n_pix), nf = uint32_t(P.frames);
                 int rk = L.rank, nr = L.nranks, tx = L.tiles_x, cw = L.width, chh = L.height;
                 float ca = L.aspect, cf = L.fov;
-                __asm__ volatile("" : "+s"(npix), "+s"(rk), "+s"(nr), "+s"(tx), "+s"(cw), "+s"(chh), "+s"(ca),
-                                 "+s"(cf));
-                const uint32_t f = i / npix, pl = i - f * npix;
+                __asm__ volatile("" : "+s"(npix), "+s"(nf), "+s"(rk), "+s"(nr), "+s"(tx), "+s"(cw), "+s"(chh),
+                                 "+s"(ca), "+s"(cf));
+                uint32_t f, pl;
+                gen_sample(nf, i, f, pl);
                 int x, y;
                 pixel_of(rk, nr, tx, pl, x, y);
                 uint32_t rg;
@@ -548,7 +564,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                 camera_ray(x, y, int32_t(uint32_t(L.frame0) + f), cw, chh, ca, cf, rg, o, d);
                 q0 = make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(d.x));
                 q1 = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), __float_as_uint(1.0f), __float_as_uint(1.0f));
-                q2 = make_uint4(__float_as_uint(1.0f), rg, i, i);
+                q2 = make_uint4(__float_as_uint(1.0f), rg, colour_slot(nf, f, pl), i);
                 q3 = make_uint4(hq.w, 0u, 0u, 0u);
             } else {
                 const PtRay *r = P.rin + hq.w;
@@ -752,7 +768,10 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
         in_lds = false;
         if (GEN && uint32_t(lane) < wcnt) {
             const uint32_t i = wbase + uint32_t(lane), npix = uint32_t(P.n_pix);
-            const uint32_t f = i / npix, pl = i - f * npix;
+            uint32_t f, pl;
+            gen_sample(uint32_t(P.frames), i, f, pl);
+            const uint32_t sid = colour_slot(uint32_t(P.frames), f, pl);  // (= i)
+            (void)npix;
             int x, y;
             pixel_of(L, pl, x, y);
             uint32_t rg;
@@ -769,7 +788,7 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
             const uint4 m = MapBounds<Map>::template mask_skip<ST>(L, o, d, skip, st);
             s0 = make_float4(o.x, o.y, o.z, d.x);
             s1 = make_float4(d.y, d.z, 1.0f, 1.0f);
-            s2 = make_float4(1.0f, __uint_as_float(rg), __uint_as_float(i), __uint_as_float(i));  // (aux: its slot)
+            s2 = make_float4(1.0f, __uint_as_float(rg), __uint_as_float(sid), __uint_as_float(i));  // (aux: its slot)
             s3 = make_uint4(m.x, m.y, 0u, 0u);
             sh = make_uint2(m.z, m.w);
         } else if (uint32_t(lane) < wcnt) {
@@ -960,31 +979,65 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
 }
 
 // fold: every pixel mixes its frames in order (test_compute.glsl:240-245).
+#define PT_FOLD_SLICE 8  // frames per LDS slice of the fold
 __device__ __forceinline__ void bin_fold_body(const PtPass &P) {
+    // A block folds PT_BIN_BLOCK consecutive local pixels.  Each pipeline's
+    // colour region holds its frames as [pixel][frame], so the block's
+    // pixels' next PT_FOLD_SLICE frames are runs of PT_FOLD_SLICE float4 per
+    // pixel: the block loads them together (8 threads per 128 B run) into
+    // LDS, then each thread mixes its pixel's frames in frame order.
+    __shared__ float4 tile[PT_BIN_BLOCK][PT_FOLD_SLICE + 1];  // (+1: no bank conflicts between rows)
     const PtLaunch &L = P.L;
-    const uint32_t pl = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pl >= uint32_t(P.n_pix) || !L.write) return;
-    int x, y;
-    pixel_of(L, pl, x, y);
-    if (x >= L.width || y >= L.height) return;
-    float4 *texel = reinterpret_cast<float4 *>(L.accum + (size_t(y) * size_t(L.width) + size_t(x)) * 4);
-    const size_t stride = size_t(P.n_pix);
-    if (L.debug != 0) {  // direct store of the chunk's (single) frame
-        const float4 c = P.color[size_t(P.frames - 1) * stride + pl];
-        *texel = make_float4(c.x, c.y, c.z, 1.0f);
+    const uint32_t t = threadIdx.x, pl0 = blockIdx.x * PT_BIN_BLOCK, pl = pl0 + t;
+    const uint32_t npix = uint32_t(P.n_pix), fr = uint32_t(P.frames);
+    const uint32_t nl = uint32_t(P.lanes > 0 ? P.lanes : 1);
+    int x = 0, y = 0;
+    bool mine = pl < npix && L.write;
+    if (mine) {
+        pixel_of(L, pl, x, y);
+        mine = x < L.width && y < L.height;
+    }
+    float4 *texel = mine ? reinterpret_cast<float4 *>(L.accum + (size_t(y) * size_t(L.width) + size_t(x)) * 4) : nullptr;
+    if (L.debug != 0) {  // direct store of the chunk's (single) frame: one pipeline, one frame
+        if (mine) {
+            const float4 c = P.color[pl];
+            *texel = make_float4(c.x, c.y, c.z, 1.0f);
+        }
         return;
     }
-    const float4 v = *texel;
-    float ar = v.x, ag = v.y, ab = v.z;
-    for (int f = 0; f < P.frames; ++f) {
-        const float4 c = P.color[size_t(f) * stride + pl];
-        const int32_t lc = int32_t(uint32_t(L.last_clear0) + uint32_t(f));
-        const float w = 1.0f / float(lc + 1), omw = 1.0f - w;
-        ar = ar * omw + c.x * w;
-        ag = ag * omw + c.y * w;
-        ab = ab * omw + c.z * w;
+    float ar = 0.0f, ag = 0.0f, ab = 0.0f;
+    if (mine) {
+        const float4 v = *texel;
+        ar = v.x;
+        ag = v.y;
+        ab = v.z;
     }
-    *texel = make_float4(ar, ag, ab, 1.0f);
+    uint32_t f0 = 0u;  // the chunk frame of region j's first frame
+    for (uint32_t j = 0u; j < nl; ++j) {
+        const uint32_t fl = fr / nl + (j < fr % nl ? 1u : 0u);
+        const float4 *reg = P.color + size_t(f0) * npix;
+        for (uint32_t s0 = 0u; s0 < fl; s0 += PT_FOLD_SLICE) {
+            const uint32_t sn = fl - s0 < PT_FOLD_SLICE ? fl - s0 : PT_FOLD_SLICE;
+            __syncthreads();  // (the previous slice's reads are done)
+            for (uint32_t e = t; e < PT_BIN_BLOCK * PT_FOLD_SLICE; e += PT_BIN_BLOCK) {
+                const uint32_t q = e / PT_FOLD_SLICE, k = e % PT_FOLD_SLICE;
+                if (k < sn && pl0 + q < npix) tile[q][k] = reg[size_t(pl0 + q) * fl + s0 + k];
+            }
+            __syncthreads();
+            if (mine) {
+                for (uint32_t k = 0u; k < sn; ++k) {
+                    const float4 c = tile[t][k];
+                    const int32_t lc = int32_t(uint32_t(L.last_clear0) + f0 + s0 + k);
+                    const float w = 1.0f / float(lc + 1), omw = 1.0f - w;
+                    ar = ar * omw + c.x * w;
+                    ag = ag * omw + c.y * w;
+                    ab = ab * omw + c.z * w;
+                }
+            }
+        }
+        f0 += fl;
+    }
+    if (mine) *texel = make_float4(ar, ag, ab, 1.0f);
 }
 
 }  // namespace pt

@@ -1004,6 +1004,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         Fp.L.spp = int32_t(fr);
         Fp.color = c->d_color;
         Fp.frames = int32_t(fr);
+        Fp.lanes = nl;  // (the colour regions' split: bin_fold_body)
         pt_launch_bin(PtBinStage::Fold, Fp, stats, unsigned((n_pix + PT_BIN_BLOCK - 1) / PT_BIN_BLOCK), c->stream);
         HIPCHK(c, hipGetLastError());
     }
