@@ -97,7 +97,8 @@ struct PtPass {
     int32_t run_max;        // trace: longest run of binned rays a wave takes at once (multiple of 64)
     int32_t refill_min;     // trace: refill when at least this many lanes are free (or none map)
     int32_t gen_order;      // gen: list the slots in generation order (idx; the host sets ctrl[0]) for the
-                            // first trace pass instead of binning them (a 64-ray window = one 8x8 tile)
+                            // first trace pass instead of binning them (the gen pass: a 64-ray window = one
+                            // 8x8 tile; gen_trace: one pixel over 64 frames, gen_sample)
     int32_t gen_trace;      // first pass without a gen pass (scene kernels, generation order): the trace
                             // pass makes each window's camera rays and bounds() itself, a miss zeroes its
                             // colour slot, and the shade pass stores (not adds) the first segment's emission
@@ -686,11 +687,13 @@ __device__ __forceinline__ void bin_scatter_body(const PtPass &P) {
 // shade pass (PtPass.hq), which reads the ray itself from its slot and
 // evaluates the normal taps (bin_shade_body).
 //
-// GEN (PtPass gen_trace, the first pass in generation order): a window's
+// GEN (PtPass gen_trace, the first pass in position order): a window's
 // rays are not loaded but made here, lane j the camera ray and bounds() mask
-// of sample wbase + j -- what gen would have written (bin_gen_body), with
-// all 64 lanes at once, stored to its slot for the shade pass -- so the
-// chunk needs no gen pass.
+// of the sample at position wbase + j (gen_sample: frame-fastest, so a
+// window is one pixel over 64 frames) -- what gen would have written
+// (bin_gen_body), with all 64 lanes at once, and, for scenes of more than 32
+// check[] entries, stored to its slot for the shade pass -- so the chunk
+// needs no gen pass.
 template <class Map, bool ST, bool TAPS = true, bool GEN = false>
 __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
     // the staged window, once its loads have landed: [part][lane], so a
