@@ -385,6 +385,50 @@ def table_kernel_leg(pt, prog, aspect: float, frames: int, steps: int = 2) -> di
         pt.set_option("jit_wait", 1)
 
 
+def edit_slot(data: np.ndarray) -> int:
+    """The data[] slot value_edit_leg nudges: the last finite value that is
+    not 0 or +-1, so a one-ulp change flips no identity flag (scale 1, zero
+    position, zero rotation axis: pt_jit.cpp) and the table kernel's source
+    stays the same -- only the values-baked build must be rebuilt."""
+    for k in range(len(data) - 1, -1, -1):
+        v = float(data[k])
+        if np.isfinite(v) and v not in (0.0, 1.0, -1.0):
+            return k
+    raise ValueError("no editable value")
+
+
+def value_edit_leg(pt, prog) -> dict:
+    """What one value edit costs an editing session (outside the timed
+    region).  The reference's edit is a buffer refresh
+    (DataArray::update, primitives.rs:131-151; sdf_editor.rs:248-252): here
+    pt_set_data uploads the table at once, the table scene kernel renders
+    from the next dispatch on (table_kernel's throughput), and the
+    values-baked build for the new values compiles on a worker thread
+    (hipRTC; the edited values' source is in no cache) and replaces it when
+    it lands.  One Float (edit_slot) is nudged by one ulp; tier_up_s is the
+    wall time from pt_set_data until that build is installed (jit_wait),
+    tier_compile_s the compile's own seconds.  Then the original values are
+    restored (their baked build comes from the shipped cache)."""
+    data = np.ascontiguousarray(prog.data, dtype=np.float32)
+    k = edit_slot(data)
+    edited = data.copy()
+    edited[k] = np.nextafter(edited[k], np.float32(np.inf))
+    pt.set_option("jit_bake", 2)
+    t0 = time.perf_counter()
+    pt.set_data(edited)
+    t1 = time.perf_counter()
+    on_table = bool(pt.get_option("jit_active")) and not pt.get_option("jit_tier_active")
+    pt.set_option("jit_wait", 1)
+    t2 = time.perf_counter()
+    out = {"tier_up_s": round(t2 - t0, 3), "tier_compile_s": round(pt.get_option("jit_tier_seconds"), 3),
+           "set_data_s": round(t1 - t0, 4), "table_kernel_meanwhile": on_table,
+           "tier_active_after": bool(pt.get_option("jit_tier_active")), "edited_slot": k,
+           "edit": "data[slot] nudged by one ulp (no identity flag flips: the table kernel is not rebuilt)"}
+    pt.set_data(data)
+    pt.set_option("jit_wait", 1)
+    return out
+
+
 def max_over_ranks(dist, v: float, device: str, op: str = "MAX") -> float:
     if dist is None:
         return v
@@ -436,36 +480,74 @@ def compare_tiles(img: np.ndarray, ref: np.ndarray, r: int, m: int) -> dict:
             "ref_zero_outside": outside_zero, "bit_exact": bad == 0 and outside_zero and bool(np.any(sel))}
 
 
+def special_tiles(img: np.ndarray, limit: int = 16) -> list:
+    """The 8x8 tiles of an image holding a texel that a sum-reduce could
+    alter: a non-finite channel (a NaN payload, an infinity: C3 and C5 hold
+    NaN texels from the reference's normalize of a zero vector)
+    or a negative zero (-0 + +0 is +0), at most `limit` of them, in tile
+    order (as test_gpu_parity.py's full-size check picks them)."""
+    h, w = img.shape[:2]
+    bits = img.view(np.uint32)
+    odd = (~np.isfinite(img)).any(axis=-1) | (bits == 0x80000000).any(axis=-1)
+    return sorted({int(t) for t in np.unique(tile_ids(w, h)[odd])})[:limit]
+
+
+def compare_one_tile(img: np.ndarray, ref: np.ndarray, t: int) -> dict:
+    """Bit-for-bit comparison of tile t of the assembled image with a render
+    of tile t alone (ref: zero outside it)."""
+    h, w = img.shape[:2]
+    ids = tile_ids(w, h)
+    sel = ids == t
+    bad = int(np.count_nonzero((img.view(np.uint32)[sel] != ref.view(np.uint32)[sel]).any(axis=-1)))
+    return {"tile": t, "texels": int(np.count_nonzero(sel)), "mismatched_texels": bad,
+            "ref_zero_outside": bool(not np.any(ref.view(np.uint32)[~sel]))}
+
+
 def validate_tiles(img: np.ndarray, prog, settings, width: int, height: int, device: int, frames: int,
-                   world: int, seed: int) -> dict:
+                   world: int, seed: int, special_limit: int = 16) -> dict:
     """Rank 0's check of the assembled (reduced) image after the timed steps:
     a fresh context renders ~8 tiles of the image -- pt_set_tiles(r, M), see
     check_tiles_spec -- over every frame the run accumulated (frame 1 ..
     frames, as TileSplitRender counts them, path_tracer.rs:110-111), and the
     texels must equal the image's bit for bit (the texel of
-    test_compute.glsl:242-245 that the reduce's sum must preserve).  Cost:
-    ~8 x 64 pixels x frames samples."""
+    test_compute.glsl:242-245 that the reduce's sum must preserve).  Then
+    every tile the image holds a non-finite or negative-zero texel in
+    (special_tiles, at most 16) is rendered alone and checked the same way:
+    the texels most likely to change in a reduce.  Cost: ~(8 + 16) x 64
+    pixels x frames samples."""
     from compute_path_tracer_amd import _native as N
     from compute_path_tracer_amd.path_tracer import PathTracer
 
     n_tiles = -(-width // 8) * -(-height // 8)
     r, m = check_tiles_spec(n_tiles, world, seed=seed)
+    special = special_tiles(img, special_limit)
     t0 = time.perf_counter()
+    c = N.Constants(time=0.0, frame=1, aspect=float(np.float32(width) / np.float32(height)), last_clear=1)
     ref = PathTracer(width, height, prog, device=device, settings=settings)
+    extra = []
     try:
         # the binned passes whatever the sample count (the automatic choice
         # would give a one-rank run's ~4 M samples to the tile-resident
         # kernel, whose ~9 waves would take seconds)
         ref.set_option("kernel", "binned")
         ref.set_tiles(r, m)
-        ref.dispatch(N.Constants(time=0.0, frame=1, aspect=float(np.float32(width) / np.float32(height)),
-                                 last_clear=1), frames)
+        ref.dispatch(c, frames)
         want = ref.read_image()
+        for t in special:  # each alone (tile t is the only one with t % n_tiles == t; set_tiles clears)
+            ref.set_tiles(t, n_tiles)
+            ref.dispatch(c, frames)
+            extra.append(compare_one_tile(img, ref.read_image(), t))
     finally:
         ref.close()
     out = compare_tiles(img, want, r, m)
+    ok = out["bit_exact"] and all(e["mismatched_texels"] == 0 and e["ref_zero_outside"] for e in extra)
     out.update({"frames": frames, "modulus": m, "residue": r,
                 "owner_ranks": sorted({t % world for t in out["tiles"]}),
+                "special_tiles": [e["tile"] for e in extra],
+                "special_owner_ranks": sorted({e["tile"] % world for e in extra}),
+                "special_texels": sum(e["texels"] for e in extra),
+                "mismatched_texels": out["mismatched_texels"] + sum(e["mismatched_texels"] for e in extra),
+                "bit_exact": bool(ok),
                 "check_s": round(time.perf_counter() - t0, 3)})
     return out
 
@@ -716,10 +798,17 @@ def main() -> None:
     kernel_ms, trace_ms, trace_n, shade_ms, shade_n = [], [], [], [], []
 
     chunks = []
+    # what the timed dispatches ran (the later legs -- solo pipeline, table
+    # kernel -- overwrite the library's read-back): whether the first pass made
+    # its own camera rays (gen_trace) and stored no ray records (gen_norec),
+    # which select the algorithmic byte model (pipeline_bytes)
+    first_pass = {}
 
     def record_times():
         kernel_ms.append(pt.last_dispatch_ms())  # whole dispatch (all pipeline kernels)
         chunks.append(int(pt.get_option("bin_chunks")))
+        first_pass["gen_trace"] = bool(pt.get_option("gen_trace"))
+        first_pass["gen_norec"] = bool(pt.get_option("gen_norec"))
         n = int(pt.get_option("trace_launches"))
         if n:  # binned pipeline: the trace / shade passes, timed by events on each pipeline's stream
             trace_ms.append(pt.get_option("trace_ms"))
@@ -761,6 +850,8 @@ def main() -> None:
     solo = solo_pipeline(pt, aspect, spp_step) if world == 1 and trace_n else None
     table = table_kernel_leg(pt, prog, aspect, spp_step) if world == 1 and trace_n and not args.no_table_kernel \
         else None
+    if table is not None:
+        table.update(value_edit_leg(pt, prog))
 
     pixels = width * height
     samples_step = pixels * spp * (world if scaling == "weak" else 1)  # all ranks
@@ -771,7 +862,7 @@ def main() -> None:
     if rank == 0:
         out = report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, spp_step, world, scaling,
                      value, ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation,
-                     solo, chunks)
+                     solo, chunks, first_pass)
         out["rccl_ranks"] = rccl_ranks
         out["reduce_backend"] = mode if world > 1 else None
         out["render_ms_per_rank"] = render
@@ -784,6 +875,11 @@ def main() -> None:
         if out is not None:
             out["c4_strong"] = leg
     if out is not None:
+        # the line says itself whether it may be trusted (a consumer reading
+        # only the JSON sees it, not just the exit status)
+        fails = validation_failures(out)
+        out["valid"] = not fails
+        out["invalid_reasons"] = fails
         print(json.dumps(out), flush=True)
     if dist is not None:
         barrier()
@@ -806,16 +902,19 @@ def exit_status(out) -> int:
 
 def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, spp_step, world, scaling, value,
            ms_step, kernel_ms, trace_ms, trace_n, shade_ms, shade_n, reduce_ms, ed, validation, solo=None,
-           chunks=None) -> dict:
-    """Rank 0's JSON line."""
+           chunks=None, first_pass=None) -> dict:
+    """Rank 0's JSON line.  first_pass: gen_trace / gen_norec
+    as the timed dispatches ran them (record_times); read back here if
+    absent."""
     d_ms = float(np.mean(kernel_ms))  # one dispatch = one step's frames of this rank
     n_chunks = float(np.mean(chunks)) if chunks else 1.0  # binned chunks per dispatch
     flops_step = algorithmic_flops(st)
     rank_pixels = st["samples"] / max(1, spp_step)
     image_bytes = 32.0 * rank_pixels  # 16 B RGBA32F load + 16 B store per pixel per dispatch
     jit = bool(pt.get_option("jit_active"))
-    gen_trace = bool(pt.get_option("gen_trace"))
-    gen_norec = bool(pt.get_option("gen_norec"))
+    fp = first_pass or {}
+    gen_trace = fp["gen_trace"] if "gen_trace" in fp else bool(pt.get_option("gen_trace"))
+    gen_norec = fp["gen_norec"] if "gen_norec" in fp else bool(pt.get_option("gen_norec"))
     pipe = pipeline_bytes(st, rank_pixels, gen_trace=gen_trace, gen_norec=gen_norec)
     shade_taps = bool(pt.get_option("shade_taps")) and jit
     n_aabb = prog.n_aabb

@@ -117,6 +117,7 @@ struct pt_ctx {
     int shade_taps = 1;                    // pt_set_option "shade_taps": normal taps in the shade pass
     int gen_trace_used = 0;                // the last timed dispatch's first pass made its own camera rays
     int gen_norec_used = 0;                // ... and stored no ray records (shade pass 0 made them again)
+    bool btab_used = false;                // the last timed binned dispatch binned by the table of check[] sets
     int cu_count = 0;
     bool fast_bounds = false;  // every box coordinate inside the reciprocal-division guard
     float bound_k = 0.0f;      // pt_bound_k of the uploaded scene (NaN: no map() bound)
@@ -703,6 +704,12 @@ static void free_bin(pt_ctx *c) {
     c->bin_cap = c->ctrl_words = 0;
 }
 
+// ensure_bin's result when the buffers' allocation itself failed (out of
+// device memory): the one failure launch_binned may answer with a smaller
+// chunk.  Any other HIP error (e.g. an earlier kernel's fault reported by the
+// synchronisation) keeps its message and ends the dispatch.
+constexpr int kBinNoMemory = -1000;
+
 // Buffers for `lanes` pipelines of `samples` samples each.
 static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
     const size_t words = size_t(PT_CTRL_STRIDE) * (passes + 1);
@@ -714,7 +721,7 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
     lanes = std::max(lanes, c->n_lanes);
     free_bin(c);
     bool ok = hipMalloc(&c->d_color, size_t(lanes) * samples * sizeof(float4)) == hipSuccess &&
-              hipMalloc(&c->d_btab, PT_BINS * sizeof(unsigned long long)) == hipSuccess;
+              hipMalloc(&c->d_btab, (PT_BINS + 1) * sizeof(unsigned long long)) == hipSuccess;  // (+ overflow count)
     for (int i = 0; ok && i < lanes; ++i) {
         pt_ctx::BinLane &l = c->lane[i];
         ok = hipMalloc(&l.ray[0], samples * sizeof(PtRay)) == hipSuccess &&
@@ -731,7 +738,8 @@ static int ensure_bin(pt_ctx *c, size_t samples, size_t passes, int lanes) {
     if (!ok) {
         free_bin(c);
         (void)hipGetLastError();
-        return fail(c, PT_ERR_HIP, "out of device memory for the binned pipeline");
+        fail(c, PT_ERR_HIP, "out of device memory for the binned pipeline");
+        return kBinNoMemory;
     }
     if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
     c->lane[0].stream = c->stream;
@@ -797,7 +805,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     };
     size_chunk();
     int rc = ensure_bin(c, size_t(n_pix) * FL, size_t(passes), lanes);
-    if (rc == PT_ERR_HIP && !c->bin_samples && !c->bin_fallback) {
+    if (rc == kBinNoMemory && !c->bin_samples && !c->bin_fallback) {
         // the total-memory size does not fit (contexts sharing the GPU):
         // size to the free memory once, fixed from now on
         c->bin_fallback = true;
@@ -806,6 +814,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         size_chunk();
         rc = ensure_bin(c, size_t(n_pix) * FL, size_t(passes), lanes);
     }
+    if (rc == kBinNoMemory) rc = PT_ERR_HIP;  // (the message is in c->err)
     if (rc != PT_OK) return rc;
     if (!stats) c->last_chunks = (spp + F - 1) / F;
     const unsigned cu = unsigned(std::max(1, c->cu_count));
@@ -820,6 +829,11 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     };
     const PtJitModule *jm = jit_active(c);
     const bool jit = jm != nullptr;
+    // the set table's overflow count covers the whole dispatch (the table
+    // itself is cleared per chunk, below)
+    const bool use_table = c->bin_table && c->n_check > uint32_t(PT_BIN_BITS) && c->n_check <= 64;
+    if (use_table) HIPCHK(c, hipMemsetAsync(c->d_btab + PT_BINS, 0, sizeof(unsigned long long), c->stream));
+    if (!stats) c->btab_used = use_table;
     // normal taps in the shade pass: march-only trace + tapping shade (scene kernels)
     const bool taps_shade = jit && c->shade_taps;
     hipFunction_t jf = jit ? (taps_shade ? (stats ? jm->trace_m_stats : jm->trace_m)
@@ -868,7 +882,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
         // the table of check[] sets starts empty per chunk (bin_resolve: only
         // scenes whose sets do not fit the bin index use it)
         unsigned long long *btab = nullptr;
-        if (c->bin_table && c->n_check > uint32_t(PT_BIN_BITS) && c->n_check <= 64) {
+        if (use_table) {
             btab = c->d_btab;
             HIPCHK(c, hipMemsetAsync(btab, 0, PT_BINS * sizeof(unsigned long long), c->stream));
         }
@@ -1326,6 +1340,20 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "bin_samples")) *value = double(bin_samples(c));
     else if (!std::strcmp(key, "bin_chunks")) *value = double(c->last_chunks);  // of the last timed binned dispatch
     else if (!std::strcmp(key, "bin_fallback")) *value = c->bin_fallback ? 1.0 : 0.0;
+    else if (!std::strcmp(key, "bin_sets") || !std::strcmp(key, "bin_overflow")) {
+        // the table of check[] sets after the last timed dispatch (-1: it did
+        // not use one): distinct sets its last chunk claimed slots for, and
+        // the sets of the whole dispatch that found no slot within
+        // PT_BIN_PROBES and shared their hash bin (pt_binned.h bin_resolve)
+        *value = -1.0;
+        if (c->btab_used && c->d_btab) {
+            std::vector<unsigned long long> t(PT_BINS + 1);
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipMemcpy(t.data(), c->d_btab, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost));
+            if (key[4] == 's') *value = double(std::count_if(t.begin(), t.end() - 1, [](unsigned long long v) { return v != 0ull; }));
+            else *value = double(t.back());
+        }
+    }
     else if (!std::strcmp(key, "trace_launches")) *value = double(c->tlog.used / 2);
     else if (!std::strcmp(key, "shade_launches")) *value = double(c->slog.used / 2);
     else if (!std::strcmp(key, "display_ms")) {

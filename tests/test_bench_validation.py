@@ -103,3 +103,43 @@ def test_exit_status_paths(capsys):
     assert bench.exit_status(_line(rccl_ranks=7)) == 1
     assert "NOT valid" in capsys.readouterr().err
     assert bench.exit_status(_line(tile_check={"bit_exact": False, "mismatched_texels": 1})) == 1
+
+
+def test_special_tiles_pick_non_finite_and_negative_zero_texels():
+    """the tiles a sum-reduce could alter -- NaN / inf
+    channels and negative zeros (-0 + +0 is +0) -- are the ones the N-GPU
+    line re-renders on top of the ~8 spread tiles, at most 16, tile order."""
+    w, h = 40, 24  # 5 x 3 tiles
+    img = np.ones((h, w, 4), np.float32)
+    assert bench.special_tiles(img) == []
+    img[3, 7, 0] = np.nan    # tile 0
+    img[20, 33, 2] = np.inf  # tile 14
+    img[9, 17, 1] = -np.inf  # tile 7
+    img[12, 2, 0] = np.float32(-0.0)  # tile 5
+    img[12, 3, 1] = np.float32(0.0)   # +0: not special
+    ids = bench.tile_ids(w, h)
+    assert bench.special_tiles(img) == sorted({int(ids[3, 7]), int(ids[20, 33]), int(ids[9, 17]), int(ids[12, 2])})
+    assert bench.special_tiles(img) == [0, 5, 7, 14]
+    assert bench.special_tiles(img, limit=2) == [0, 5]
+    # a NaN in every tile: the first 16
+    many = np.ones((64, 64, 4), np.float32)
+    many[::8, ::8, 3] = np.nan
+    assert bench.special_tiles(many) == list(range(16))
+
+
+def test_compare_one_tile():
+    w, h = 40, 24
+    rng = np.random.default_rng(1)
+    img = rng.standard_normal((h, w, 4)).astype(np.float32)
+    img[9, 17, 0] = np.nan
+    t = int(bench.tile_ids(w, h)[9, 17])
+    sel = bench.tile_ids(w, h) == t
+    ref = np.where(sel[..., None], img, np.float32(0.0)).astype(np.float32)
+    ok = bench.compare_one_tile(img, ref, t)
+    assert ok == {"tile": t, "texels": 64, "mismatched_texels": 0, "ref_zero_outside": True}
+    bad = ref.copy()
+    bad.view(np.uint32)[9, 17, 0] ^= np.uint32(0x80000000)  # the same NaN with its sign bit flipped
+    assert bench.compare_one_tile(img, bad, t)["mismatched_texels"] == 1
+    leak = ref.copy()
+    leak[0, 0, 0] = 1.0
+    assert not bench.compare_one_tile(img, leak, t)["ref_zero_outside"]

@@ -74,6 +74,24 @@ def test_default_line_checks_its_tiles(gpu):
     assert bench_exit_ok(out)
 
 
+@pytest.mark.timeout(600)
+def test_line_checks_non_finite_tiles(gpu):
+    """the N > 1 line also re-renders every tile of the
+    assembled image that holds a non-finite or negative-zero texel
+    (bench.special_tiles) -- the texels a reduce's sum is most likely to
+    alter.  C3 at 1080p holds NaN texels from its first 256 frames on (the
+    reference's normalize of a zero vector), so a
+    two-rank line over frames 1..512 must list them and match bit for bit."""
+    out = _bench("--spp", "128", "--steps", "1", "--warmup", "0", "--c4-steps", "0")
+    tc = out["tile_check"]
+    assert tc["frames"] == (0 + 1 + 1) * 128 * 2
+    assert len(tc["special_tiles"]) >= 1, tc
+    assert tc["special_texels"] == 64 * len(tc["special_tiles"])
+    assert set(tc["special_owner_ranks"]) <= {0, 1}
+    assert tc["bit_exact"] is True and tc["mismatched_texels"] == 0
+    assert out["valid"] is True and out["invalid_reasons"] == []
+
+
 def bench_exit_ok(out: dict) -> bool:
     sys.path.insert(0, ROOT)
     import bench
