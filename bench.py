@@ -212,6 +212,87 @@ def profiled(config: dict):
     return best
 
 
+PEAK_F32_NO_FMA_TFLOPS = PEAK_F32_TFLOPS / 2.0  # one flop per lane-op: the ceiling without FMA contraction
+
+
+def flop_calibration():
+    """The newest committed executed-flop calibration
+    (profiles/*_flop_calibration.json, scripts/flop_calib.py: FP32 flops
+    per counted event fitted to PMC instruction counts over scenes x
+    bounces) as (calibration, path); None if there is none."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_flop_calibration.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("classes"):
+            best = (d, os.path.relpath(f, ROOT))
+    return best
+
+
+def calibrated_flops(cal: dict, cls: str, st: dict, taps: dict, n_aabb: int) -> tuple:
+    """(executed flops, {event: (count, executed flops, SURVEY-weight
+    flops)}) of one kernel class over a dispatch's counters, at the
+    calibration's fitted weights."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from flop_calib import features
+
+    c = cal["classes"][cls]
+    x = features(st, taps, n_aabb)[cls]
+    by = {k: (x[k], x[k] * w, x[k] * c["survey_weights"][k]) for k, w in c["executed_flops_per_event"].items()}
+    return float(sum(v[1] for v in by.values())), by
+
+
+def measured_view(pmc_flops, pk: dict, src: str, time_ms: float, cal, cls: str, st: dict, taps: dict, n_aabb: int,
+                  survey_frac: float) -> dict:
+    """roofline.measured: what the hardware did in the dominant kernel class
+    (VERDICT r05 item 3), over the same solo launches as roofline.frac
+    (time_ms: their summed HIP-event time).  pmc_flops: the FP32 flops of
+    those launches by the kernels' own instruction counts in the
+    one-pipeline PMC profile (add / mul 1, fma 2 per lane, at each kernel's
+    lane utilisation; scaled to this run's launch size); pk: the dominant
+    kernel's derived counters there (VALU issue, lane utilisation, lane-slots
+    busy).  The contract leaves almost no FMAs (no contraction),
+    so a lane-op carries <= 1 flop: half the FP32 peak, 78.65 TFLOP/s, is
+    the no-FMA ceiling.  From the calibration (cal): the counted events at
+    their fitted executed weights over the same time --
+    frac_executed_calibrated, the SURVEY-weight frac (survey_frac)
+    reconciled with the PMC instruction classes -- and the per-event split."""
+    out = {"peak": PEAK_F32_TFLOPS, "no_fma_ceiling": PEAK_F32_NO_FMA_TFLOPS, "unit": "TFLOP/s",
+           "kernel_class": cls, "frac_survey_weights": survey_frac}
+    if pmc_flops and time_ms:
+        tf = pmc_flops / (time_ms * 1e-3) / 1e12
+        out.update({"fp32_tflops_pmc": round(tf, 3), "fp32_frac_pmc": round(tf / PEAK_F32_TFLOPS, 4),
+                    "fp32_frac_of_no_fma_ceiling": round(tf / PEAK_F32_NO_FMA_TFLOPS, 4)})
+    if pk:
+        hv = hw_view(pk)
+        for k in ("valu_issue_frac_of_peak", "valu_lane_utilization", "valu_lane_slots_busy", "wave_time_waitcnt"):
+            if k in hv:
+                out[k] = hv[k]
+        if pk.get("fp32_insts_frac_of_valu") is not None:
+            out["fp32_insts_frac_of_valu"] = round(pk["fp32_insts_frac_of_valu"], 4)
+        out["pmc_source"] = f"{src} (one pipeline, per launch, scaled to this run's launch size; time: this run's solo launches)"
+    if cal is not None and time_ms:
+        c, csrc = cal
+        fl, by = calibrated_flops(c, cls, st, taps, n_aabb)
+        tf = fl / (time_ms * 1e-3) / 1e12
+        cc = c["classes"][cls]
+        out.update({"tflops_executed_calibrated": round(tf, 3), "frac_executed_calibrated": round(tf / PEAK_F32_TFLOPS, 4),
+                    "calibration_source": f"{csrc} (scripts/flop_calib.py: NNLS of PMC FP32 flops on the counted "
+                                          f"events over {c.get('configs')} scene x bounce configurations; rms relative "
+                                          f"residual {cc.get('rms_rel_residual')})",
+                    "by_event": {k: {"count": int(v[0]), "executed_flops_per_event": cc["executed_flops_per_event"][k],
+                                     "survey_flops_per_event": cc["survey_weights"][k],
+                                     "executed_share": round(v[1] / fl, 4) if fl else None}
+                                 for k, v in by.items()}})
+        if out.get("fp32_tflops_pmc"):
+            out["calibrated_over_pmc"] = round(tf / out["fp32_tflops_pmc"], 4)
+    return out
+
+
 def hw_view(derived: dict) -> dict:
     """The hardware counters' view of a kernel beside its algorithmic frac:
     VALU issue (fraction of the wave64 issue rate) x lane utilisation = the
@@ -385,16 +466,16 @@ def table_kernel_leg(pt, prog, aspect: float, frames: int, steps: int = 2) -> di
         pt.set_option("jit_wait", 1)
 
 
-def edit_slot(data: np.ndarray) -> int:
-    """The data[] slot value_edit_leg nudges: the last finite value that is
-    not 0 or +-1, so a one-ulp change flips no identity flag (scale 1, zero
-    position, zero rotation axis: pt_jit.cpp) and the table kernel's source
-    stays the same -- only the values-baked build must be rebuilt."""
-    for k in range(len(data) - 1, -1, -1):
-        v = float(data[k])
-        if np.isfinite(v) and v not in (0.0, 1.0, -1.0):
-            return k
-    raise ValueError("no editable value")
+def edit_slot(prog) -> int:
+    """The data[] slot value_edit_leg nudges: the first shape's size -- a
+    value the generated map() uses (so the values-baked source changes) and
+    no identity flag depends on (those are scale 1, zero position and zero
+    rotation axis: pt_jit.cpp), so the table kernel's source stays the same
+    and only the values-baked build is rebuilt."""
+    for o in prog.op_dicts():
+        if o["opcode"] == 1 and np.isfinite(float(prog.data[o["size"][0]])):  # PT_OP_SHAPE
+            return int(o["size"][0])
+    raise ValueError("no shape")
 
 
 def value_edit_leg(pt, prog) -> dict:
@@ -410,7 +491,7 @@ def value_edit_leg(pt, prog) -> dict:
     tier_compile_s the compile's own seconds.  Then the original values are
     restored (their baked build comes from the shipped cache)."""
     data = np.ascontiguousarray(prog.data, dtype=np.float32)
-    k = edit_slot(data)
+    k = edit_slot(prog)
     edited = data.copy()
     edited[k] = np.nextafter(edited[k], np.float32(np.inf))
     pt.set_option("jit_bake", 2)
@@ -423,7 +504,8 @@ def value_edit_leg(pt, prog) -> dict:
     out = {"tier_up_s": round(t2 - t0, 3), "tier_compile_s": round(pt.get_option("jit_tier_seconds"), 3),
            "set_data_s": round(t1 - t0, 4), "table_kernel_meanwhile": on_table,
            "tier_active_after": bool(pt.get_option("jit_tier_active")), "edited_slot": k,
-           "edit": "data[slot] nudged by one ulp (no identity flag flips: the table kernel is not rebuilt)"}
+           "edit": "a shape size (data[edited_slot]) nudged by one ulp: no identity flag flips, so the table "
+                   "kernel is not rebuilt; the values-baked build is"}
     pt.set_data(data)
     pt.set_option("jit_wait", 1)
     return out
@@ -824,6 +906,11 @@ def main() -> None:
     pt.sync()
     barrier()
     dt = max_over_ranks(dist, time.perf_counter() - t0, dev)
+    # the table of check[] sets after the last timed dispatch:
+    # the distinct sets its last chunk saw (of PT_BINS slots) and the sets
+    # that found no slot and shared a hash bin (-1: no table in use)
+    bin_table = {"slots": 4096, "sets_last_chunk": int(pt.get_option("bin_sets")),
+                 "overflow": int(pt.get_option("bin_overflow"))}
     if world > 1:
         # per-launch kernel time on this rank (events on the library stream)
         tr.step(spp)
@@ -867,6 +954,7 @@ def main() -> None:
         out["reduce_backend"] = mode if world > 1 else None
         out["render_ms_per_rank"] = render
         out["tile_check"] = tile_check
+        out["schedule"]["bin_table"] = bin_table
         if table is not None:
             out["table_kernel"] = table
     pt.close()
@@ -1110,6 +1198,16 @@ def report(args, pt, st, taps, prog, scene_name, width, height, bounces, spp, sp
         out["hbm"]["trace_kernel_measured_bytes_per_launch"] = out["roofline"].get("traffic")
         if tk:
             out["roofline"]["hw"] = dict(hw_view(tk), source=src)
+        if solo is not None and tk.get("fp32_flops_per_launch"):
+            # the solo dispatch's trace launches: one first pass per chunk, the
+            # rest march-only (one pipeline)
+            n_g = float(solo.get("chunks", n_chunks)) if gen_trace else 0.0
+            n_m = max(0.0, float(solo["trace_n"]) - n_g)
+            pmc = tk["fp32_flops_per_launch"] * scale * n_m + \
+                (first.get("fp32_flops_per_launch", 0.0) * scale * n_g if gen_trace else 0.0)
+            out["roofline"]["measured"] = measured_view(
+                pmc, tk, src, solo["trace_ms"], flop_calibration(), "trace", solo["st"], solo["taps"], n_aabb,
+                out["roofline"]["frac"])
         if sk:
             out["roofline"]["shade"]["hw"] = dict(hw_view(sk), source=src)
     if not args.no_cpu_baseline and world == 1:

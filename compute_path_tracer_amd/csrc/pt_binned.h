@@ -103,6 +103,7 @@ struct PtPass {
     int32_t gen_trace;      // first pass without a gen pass (scene kernels, generation order): the trace
                             // pass makes each window's camera rays and bounds() itself, a miss zeroes its
                             // colour slot, and the shade pass stores (not adds) the first segment's emission
+    int32_t count_overflow; // bin_resolve counts the sets that find no slot (btab[PT_BINS]; instrumented runs)
     int32_t gen_norec;      // gen_trace, check[] of <= 32 entries: the first pass writes no ray records -- its
                             // hit quads carry the ray's check[] bits in .w (the slot is the position) -- and
                             // shade pass 0 makes each traced camera ray again (camera_ray: the same bits)
@@ -166,7 +167,9 @@ __device__ __forceinline__ uint32_t bin_resolve(const PtPass &P, const uint4 &m,
         if (v == 0ull) v = atomicCAS(P.btab + s, 0ull, b.e);
         if (v == 0ull || v == b.e) return s;
         if (++k == PT_BIN_PROBES) {  // no slot for this set: it shares its hash bin
-            atomicAdd(P.btab + PT_BINS, 1ull);  // (the overflow count, pt_get_option "bin_overflow")
+            // (counted by the instrumented dispatch only: one word that every
+            // overflowing lane adds to would be a hot atomic in the timed one)
+            if (P.count_overflow) atomicAdd(P.btab + PT_BINS, 1ull);
             return b.h;
         }
         s = (s + 1u) & uint32_t(PT_BINS - 1);

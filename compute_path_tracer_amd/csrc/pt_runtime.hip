@@ -118,6 +118,7 @@ struct pt_ctx {
     int gen_trace_used = 0;                // the last timed dispatch's first pass made its own camera rays
     int gen_norec_used = 0;                // ... and stored no ray records (shade pass 0 made them again)
     bool btab_used = false;                // the last timed binned dispatch binned by the table of check[] sets
+    bool btab_counted = false;             // the last instrumented one did, and counted its overflows
     int cu_count = 0;
     bool fast_bounds = false;  // every box coordinate inside the reciprocal-division guard
     float bound_k = 0.0f;      // pt_bound_k of the uploaded scene (NaN: no map() bound)
@@ -832,8 +833,9 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
     // the set table's overflow count covers the whole dispatch (the table
     // itself is cleared per chunk, below)
     const bool use_table = c->bin_table && c->n_check > uint32_t(PT_BIN_BITS) && c->n_check <= 64;
-    if (use_table) HIPCHK(c, hipMemsetAsync(c->d_btab + PT_BINS, 0, sizeof(unsigned long long), c->stream));
+    if (use_table && stats) HIPCHK(c, hipMemsetAsync(c->d_btab + PT_BINS, 0, sizeof(unsigned long long), c->stream));
     if (!stats) c->btab_used = use_table;
+    if (stats) c->btab_counted = use_table;
     // normal taps in the shade pass: march-only trace + tapping shade (scene kernels)
     const bool taps_shade = jit && c->shade_taps;
     hipFunction_t jf = jit ? (taps_shade ? (stats ? jm->trace_m_stats : jm->trace_m)
@@ -912,6 +914,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             p.frames = int32_t(fl[i]);
             p.wide = c->n_check > 64 ? 1 : 0;
             p.btab = btab;
+            p.count_overflow = stats ? 1 : 0;
             p.run_max = run_max;
             p.refill_min = refill_min;
         }
@@ -1341,16 +1344,18 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
     else if (!std::strcmp(key, "bin_chunks")) *value = double(c->last_chunks);  // of the last timed binned dispatch
     else if (!std::strcmp(key, "bin_fallback")) *value = c->bin_fallback ? 1.0 : 0.0;
     else if (!std::strcmp(key, "bin_sets") || !std::strcmp(key, "bin_overflow")) {
-        // the table of check[] sets after the last timed dispatch (-1: it did
-        // not use one): distinct sets its last chunk claimed slots for, and
-        // the sets of the whole dispatch that found no slot within
-        // PT_BIN_PROBES and shared their hash bin (pt_binned.h bin_resolve)
+        // the table of check[] sets (-1: not in use): bin_sets, the distinct
+        // sets the last chunk of the last dispatch claimed slots for;
+        // bin_overflow, the lookups of the last instrumented dispatch
+        // (pt_dispatch_stats) whose set found no slot within PT_BIN_PROBES
+        // and shared its hash bin (pt_binned.h bin_resolve)
         *value = -1.0;
-        if (c->btab_used && c->d_btab) {
+        const bool sets = key[4] == 's';
+        if ((sets ? c->btab_used : c->btab_counted) && c->d_btab) {
             std::vector<unsigned long long> t(PT_BINS + 1);
             HIPCHK(c, hipStreamSynchronize(c->stream));
             HIPCHK(c, hipMemcpy(t.data(), c->d_btab, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost));
-            if (key[4] == 's') *value = double(std::count_if(t.begin(), t.end() - 1, [](unsigned long long v) { return v != 0ull; }));
+            if (sets) *value = double(std::count_if(t.begin(), t.end() - 1, [](unsigned long long v) { return v != 0ull; }));
             else *value = double(t.back());
         }
     }

@@ -121,3 +121,35 @@ def test_executed_flops_drop_only_culled_work(counters):
     assert ex[0] < alg[0] and ex[1] == pytest.approx(alg[1])
     per = bench.W_XFORM + bench.W_FINALISE + 1 - bench.W_CULL_TEST
     assert alg[0] - ex[0] >= st_c["culled"] * per  # (plus the mean SDF weight)
+
+
+def _kernel_source(prog, data, baked: int) -> str:
+    import ctypes
+
+    from compute_path_tracer_amd import _native as N
+
+    d = np.ascontiguousarray(data, np.float32)
+    args = (prog.ops, prog.n_ops, prog.aabbs, prog.n_aabb, d.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(d),
+            baked)
+    n = ctypes.c_size_t()
+    assert N.lib().pt_scene_kernel_source(*args, None, 0, ctypes.byref(n)) == N.PT_OK
+    buf = ctypes.create_string_buffer(n.value)
+    assert N.lib().pt_scene_kernel_source(*args, buf, n.value, ctypes.byref(n)) == N.PT_OK
+    return buf.value.decode()
+
+
+@pytest.mark.parametrize("scene", ["c1", "c2", "c3"])
+def test_value_edit_leg_rebuilds_only_the_baked_kernel(scene):
+    """bench.value_edit_leg's one-ulp edit: the table
+    scene kernel's source is unchanged (no recompile: what an editing
+    session renders meanwhile) and the values-baked source differs (its
+    rebuild is what tier_up_s times -- a source no cache holds)."""
+    from compute_path_tracer_amd import scenes
+    from compute_path_tracer_amd.sdf_editor import CompData
+
+    prog = scenes.SCENES[scene]().compile(CompData())
+    k = bench.edit_slot(prog)
+    edited = prog.data.astype(np.float32).copy()
+    edited[k] = np.nextafter(edited[k], np.float32(np.inf))
+    assert _kernel_source(prog, prog.data, 0) == _kernel_source(prog, edited, 0)
+    assert _kernel_source(prog, prog.data, 1) != _kernel_source(prog, edited, 1)

@@ -181,3 +181,45 @@ def test_launch_split(tmp_path):
     assert ls["shade_solo_ms"] == pytest.approx(0.5e-3)
     assert ls["trace_timed_ms"] == pytest.approx(3e-3)
     assert ls["shade_timed_ms"] == pytest.approx(1e-3)
+
+
+def test_measured_view_pmc_and_calibration(frame, tmp_path, monkeypatch):
+    """roofline.measured: the PMC FP32 flops of the
+    solo trace launches (8 march launches + 1 first pass, per-launch figures
+    of a one-pipeline profile halved for this two-pipeline run's launch size)
+    over their time, the no-FMA ceiling, and the counted events at a
+    calibration's executed weights (frac_executed_calibrated, by_event)."""
+    out0 = _report(frame)
+    cfg = {k: out0["config"][k] for k in ("width", "height", "bounces", "spp_per_step", "workload")}
+    pmc = {"bench_config": dict(cfg, pipelines=1),
+           "per_kernel": {"pt_bin_trace_m_jit": {"hbm_bytes_per_launch": 1.0, "fp32_flops_per_launch": 4.0e9,
+                                                 "valu_issue_frac_of_peak": 0.8, "valu_lane_utilization": 0.7,
+                                                 "fp32_insts_frac_of_valu": 0.5},
+                          "pt_bin_trace_g_jit": {"hbm_bytes_per_launch": 1.0, "fp32_flops_per_launch": 6.0e9}}}
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "zz_pmc.json").write_text(json.dumps(pmc))
+    import flop_calib
+
+    ev = {"march_steps": 3.0, "xform_union": 20.0, "shape_evals": 30.0, "culled": 5.0, "samples": 40.0,
+          "primary_box_tests": 10.0}
+    cal = {"configs": 24, "classes": {"trace": {"executed_flops_per_event": ev, "rms_rel_residual": 0.01,
+                                                "survey_weights": {k: 1.0 for k in ev}},
+                                      "shade": {"executed_flops_per_event": {}, "survey_weights": {}}}}
+    (tmp_path / "profiles" / "zz_flop_calibration.json").write_text(json.dumps(cal))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    r = _report(frame)["roofline"]
+    m = r["measured"]
+    pmc_flops = 4.0e9 * 0.5 * 8 + 6.0e9 * 0.5 * 1
+    assert m["fp32_tflops_pmc"] == pytest.approx(pmc_flops / 1.5e-3 / 1e12, abs=5e-4)
+    assert m["no_fma_ceiling"] == pytest.approx(bench.PEAK_F32_TFLOPS / 2)
+    assert m["fp32_frac_of_no_fma_ceiling"] == pytest.approx(2 * m["fp32_frac_pmc"], abs=2e-4)
+    assert m["valu_lane_slots_busy"] == pytest.approx(0.56)
+    _, prog, st, taps = frame
+    x = flop_calib.features(st, taps, prog.n_aabb)["trace"]
+    fl = sum(ev[k] * x[k] for k in ev)
+    assert m["tflops_executed_calibrated"] == pytest.approx(fl / 1.5e-3 / 1e12, abs=5e-4)
+    assert m["frac_executed_calibrated"] == pytest.approx(fl / 1.5e-3 / 1e12 / bench.PEAK_F32_TFLOPS, abs=1e-4)
+    assert m["frac_survey_weights"] == r["frac"]
+    assert set(m["by_event"]) == set(ev) and sum(v["executed_share"] for v in m["by_event"].values()) == \
+        pytest.approx(1.0, abs=1e-3)
+    assert m["calibration_source"].startswith(os.path.join("profiles", "zz_flop_calibration.json"))
