@@ -330,62 +330,13 @@ __device__ __forceinline__ uint64_t primary_box_skip(const PtLaunch &L, const pt
     return __ballot(skip);
 }
 
-// Non-temporal store hints (A/B experiments, PT_JIT_DEFS; off by default:
-// PT_ST then expands to the plain assignment, so the shipped code is unchanged).
-typedef unsigned int pt_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void nt_quad(uint4 *p, const uint4 &v) {
-    __builtin_nontemporal_store(pt_u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<pt_u32x4 *>(p));
-}
-__device__ __forceinline__ void nt_quad(float4 *p, const float4 &v) {
-    nt_quad(reinterpret_cast<uint4 *>(p),
-            make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)));
-}
-__device__ __forceinline__ void nt_quad(uint32_t *p, uint32_t v) { __builtin_nontemporal_store(v, p); }
-#define PT_ST(ptr, val, nt)            \
-    do {                               \
-        if (nt) nt_quad((ptr), (val)); \
-        else *(ptr) = (val);           \
-    } while (0)
-#ifdef PT_NT_RAY  // the shade pass's next rays
-#define PT_NT_RAY_ON true
-#else
-#define PT_NT_RAY_ON false
-#endif
-#ifdef PT_NT_KEY  // the shade pass's bin keys
-#define PT_NT_KEY_ON true
-#else
-#define PT_NT_KEY_ON false
-#endif
-#ifdef PT_NT_COLOR  // the shade pass's colour-slot stores
-#define PT_NT_COLOR_ON true
-#else
-#define PT_NT_COLOR_ON false
-#endif
-#ifdef PT_NT_HQ  // the march pass's hit quads
-#define PT_NT_HQ_ON true
-#else
-#define PT_NT_HQ_ON false
-#endif
-
 __device__ __forceinline__ void store_ray(PtRay *r, const pt_f3 &ro, const pt_f3 &rd, const pt_f3 &thr, uint32_t rng,
-                                          uint32_t sid, uint32_t aux, const uint4 &q3, bool nt = false) {
-    PT_ST(&r->q[0], make_uint4(__float_as_uint(ro.x), __float_as_uint(ro.y), __float_as_uint(ro.z), __float_as_uint(rd.x)),
-          nt);
-    PT_ST(&r->q[1], make_uint4(__float_as_uint(rd.y), __float_as_uint(rd.z), __float_as_uint(thr.x), __float_as_uint(thr.y)),
-          nt);
-    PT_ST(&r->q[2], make_uint4(__float_as_uint(thr.z), rng, sid, aux), nt);
-    PT_ST(&r->q[3], q3, nt);
+                                          uint32_t sid, uint32_t aux, const uint4 &q3) {
+    r->q[0] = make_uint4(__float_as_uint(ro.x), __float_as_uint(ro.y), __float_as_uint(ro.z), __float_as_uint(rd.x));
+    r->q[1] = make_uint4(__float_as_uint(rd.y), __float_as_uint(rd.z), __float_as_uint(thr.x), __float_as_uint(thr.y));
+    r->q[2] = make_uint4(__float_as_uint(thr.z), rng, sid, aux);
+    r->q[3] = q3;
 }
-
-// A wave's 64 consecutive entries of an array as a buffer resource (base =
-// the wave's first entry, wave-uniform): a store at a lane offset beyond
-// `bytes` is dropped by the hardware's range check, so a per-lane store
-// needs no branch and no exec-mask region (pt_binned.h bin_shade_body's
-// deferred stores: the compiler's vmcnt waits stay exact behind them).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void *base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), short(0), int(bytes), 0x00020000);
-}
-#define PT_OOB 0x40000000u  // a lane offset outside every wave_rsrc range
 
 __device__ __forceinline__ void hist_zero(uint32_t *lh) {
     for (int b = int(threadIdx.x); b < PT_BINS; b += int(blockDim.x)) lh[b] = 0u;
@@ -501,45 +452,6 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     stt.init();
     const PtLaunch &L = P.L;
     const uint32_t n = P.n_src ? *P.n_src : P.n_src_const;
-    // Deferred stores (TAPS = false, PT_SHADE_DEFER): a position's next ray
-    // and key are kept in registers and stored after the NEXT position's hit
-    // quad and ray loads have been issued.  gfx9's vmcnt retires loads and
-    // stores in one in-order count, so a load issued behind a position's
-    // five stores waits for them as well: stored at the end of the position,
-    // they were drained at the next loop head by its quad load (vmcnt(0)).
-    // Issued behind the loads, they complete while the gather is in flight,
-    // and the gather's wait skips them (vmcnt(5)).  The stores go through a
-    // buffer resource over the wave's 64 positions, a lane without a ray
-    // (an ended path, the first position) at an offset the range check
-    // drops: no branch, so the compiler's wait counts stay exact.
-#ifdef PT_SHADE_DEFER
-    constexpr bool kDefer = !TAPS;
-#else
-    constexpr bool kDefer = false;
-#endif
-    constexpr uint32_t kNoPos = 0xffffffffu;
-    struct Pend {
-        uint32_t pos, key;  // pos kNoPos: nothing pending; key PT_BIN_NONE: no ray (the key is stored anyway)
-        pt_f3 ro, rd, thr;
-        uint32_t rng, sid, mx, my;
-    } pd;
-    // every path of a position sets every field (an ended path or a miss
-    // with values it has at hand), so nothing of the previous position stays
-    // live across the next one's body
-    auto pd_set = [&](uint32_t key, const pt_f3 &ro, const pt_f3 &rd, const pt_f3 &thr, uint32_t rng, uint32_t sid,
-                      uint32_t mx, uint32_t my) {
-        pd.key = key;
-        pd.ro = ro;
-        pd.rd = rd;
-        pd.thr = thr;
-        pd.rng = rng;
-        pd.sid = sid;
-        pd.mx = mx;
-        pd.my = my;
-    };
-    const pt_f3 f0{0.0f, 0.0f, 0.0f};
-    pd.pos = kNoPos;
-    pd_set(PT_BIN_NONE, f0, f0, f0, 0u, 0u, 0u, 0u);
     // q0..q3: the traced ray (TAPS = false; hq its hit quad) or the hit
     // record (TAPS = true)
     auto shade_one = [&](uint32_t i, const uint4 &q0, const uint4 &q1, const uint4 &q2, const uint4 &q3,
@@ -597,65 +509,29 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         // never holds -0), and a zero e changes no slot, so only emitting
         // segments touch it
         if (P.gen_trace) {  // first segment, no gen pass: the slot was never zeroed; 0 + e = e
-            PT_ST(P.color + sid, make_float4(ret.x, ret.y, ret.z, 0.0f), PT_NT_COLOR_ON);
+            P.color[sid] = make_float4(ret.x, ret.y, ret.z, 0.0f);
         } else if (ret.x != 0.0f || ret.y != 0.0f || ret.z != 0.0f) {
             float4 c = P.color[sid];
             c.x += ret.x;
             c.y += ret.y;
             c.z += ret.z;
-            PT_ST(P.color + sid, c, PT_NT_COLOR_ON);
+            P.color[sid] = c;
         }
         if (done) {
             if (L.debug == 3) {  // bounce-count view: the colour is the segment count, not the radiance
                 const pt_f3 col = final_color(L.debug, seg, L.bounces, ret);
                 P.color[sid] = make_float4(col.x, col.y, col.z, 0.0f);
             }
-            if constexpr (kDefer) pd_set(PT_BIN_NONE, ro, rd, thr, rng, sid, 0u, 0u);  // (no ray: its fields unused)
-            else PT_ST(P.key + i, PT_BIN_NONE, PT_NT_KEY_ON);
+            P.key[i] = PT_BIN_NONE;
             return;
         }
         const uint4 m = MapBounds<Map>::template mask<ST>(L, ro, rd, st);
         const BinProbe bp = bin_probe(P, m);  // (before the stores: bin_probe)
-        if constexpr (kDefer) {
-            pd_set(PT_BIN_NONE, ro, rd, thr, rng, sid, m.x, m.y);  // (the key below)
-        } else {
-            store_ray(P.rout + i, ro, rd, thr, rng, sid, i, make_uint4(m.x, m.y, 0u, 0u), PT_NT_RAY_ON);
-        }
+        store_ray(P.rout + i, ro, rd, thr, rng, sid, i, make_uint4(m.x, m.y, 0u, 0u));
         if (wide_of<Map>(P)) P.mask_hi[i] = make_uint2(m.z, m.w);
         const uint32_t k = bin_resolve(P, m, bp);
-        if constexpr (kDefer) pd.key = k;
-        else PT_ST(P.key + i, k, PT_NT_KEY_ON);
+        P.key[i] = k;
         atomicAdd(&lh[k], 1u);
-    };
-    // kDefer: the pending ray and key of each lane's previous position, in
-    // the loop (every active lane has one, or none has: the first position),
-    // as predicated buffer stores over the wave's 64 positions
-    auto flush_wave = [&]() {
-        const uint32_t lane = threadIdx.x & 63u;
-        const bool pv = pd.pos != kNoPos;
-        const uint32_t w0 = uint32_t(__builtin_amdgcn_readfirstlane(int(pv ? pd.pos - lane : 0u)));
-        const __amdgpu_buffer_rsrc_t rr = wave_rsrc(P.rout + w0, 64u * uint32_t(sizeof(PtRay)));
-        const __amdgpu_buffer_rsrc_t kr = wave_rsrc(P.key + w0, 64u * 4u);
-        const uint32_t ro_off = pv && pd.key != PT_BIN_NONE ? lane * uint32_t(sizeof(PtRay)) : PT_OOB;
-        const uint32_t ko_off = pv ? lane * 4u : PT_OOB;
-        const pt_u32x4 a = {__float_as_uint(pd.ro.x), __float_as_uint(pd.ro.y), __float_as_uint(pd.ro.z),
-                            __float_as_uint(pd.rd.x)};
-        const pt_u32x4 b = {__float_as_uint(pd.rd.y), __float_as_uint(pd.rd.z), __float_as_uint(pd.thr.x),
-                            __float_as_uint(pd.thr.y)};
-        const pt_u32x4 c = {__float_as_uint(pd.thr.z), pd.rng, pd.sid, pd.pos};  // (aux: the ray's slot)
-        const pt_u32x4 d = {pd.mx, pd.my, 0u, 0u};
-        __builtin_amdgcn_raw_buffer_store_b128(a, rr, int(ro_off), 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(b, rr, int(ro_off), 16, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(c, rr, int(ro_off), 32, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(d, rr, int(ro_off), 48, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(pd.key, kr, int(ko_off), 0, 0);
-    };
-    // after the loop: the lanes' last positions (plain stores)
-    auto flush_last = [&]() {
-        if (pd.pos == kNoPos) return;
-        if (pd.key != PT_BIN_NONE)
-            store_ray(P.rout + pd.pos, pd.ro, pd.rd, pd.thr, pd.rng, pd.sid, pd.pos, make_uint4(pd.mx, pd.my, 0u, 0u));
-        P.key[pd.pos] = pd.key;
     };
     // One thread per binned position.  TAPS = false: its hit quad, then the
     // traced ray from the quad's slot; TAPS = true: its hit record (a miss
@@ -671,27 +547,11 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             // the compiler loads .yz, tests, then loads .xw inside the
             // branch -- a second round trip before the ray's gather)
             __asm__ volatile("" : "+v"(hq.x), "+v"(hq.y), "+v"(hq.z), "+v"(hq.w));
-            uint4 q0, q1, q2, q3;
-            if constexpr (kDefer) {
-                // the traced ray's gather, then the previous position's stores
-                const bool hit = hq.y != PT_AUX_MISS;
-                if (hit && !P.gen_norec) {
-                    const PtRay *r = P.rin + hq.w;
-                    q0 = r->q[0];
-                    q1 = r->q[1];
-                    q2 = r->q[2];
-                    q3 = r->q[3];
-                }
-                flush_wave();
-                pd.pos = i;
-                if (!hit) {
-                    pd_set(PT_BIN_NONE, f0, f0, f0, 0u, 0u, 0u, 0u);  // the path ended in the trace pass
-                    continue;
-                }
-            } else if (hq.y == PT_AUX_MISS) {
-                PT_ST(P.key + i, PT_BIN_NONE, PT_NT_KEY_ON);  // the path ended in the trace pass
+            if (hq.y == PT_AUX_MISS) {
+                P.key[i] = PT_BIN_NONE;  // the path ended in the trace pass
                 continue;
             }
+            uint4 q0, q1, q2, q3;
             if (P.gen_norec) {
                 // shade pass 0 without ray records: the traced camera ray of
                 // sample i (its slot is its position) made again, as the first
@@ -717,7 +577,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                 q1 = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), __float_as_uint(1.0f), __float_as_uint(1.0f));
                 q2 = make_uint4(__float_as_uint(1.0f), rg, colour_slot(nf, f, pl), i);
                 q3 = make_uint4(hq.w, 0u, 0u, 0u);
-            } else if constexpr (!kDefer) {  // (kDefer: gathered above)
+            } else {
                 const PtRay *r = P.rin + hq.w;
                 q0 = r->q[0];
                 q1 = r->q[1];
@@ -732,7 +592,6 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
             shade_one(i, q0, q1, q2, q3, hi, hq);
         }
     }
-    if constexpr (kDefer) flush_last();
     hist_flush(lh, P.hist);
     flush_stats<ST>(L, st);
     if constexpr (!TAPS) flush_stats<ST>(L, stt, PT_ST_COUNT);
@@ -979,17 +838,15 @@ __device__ __forceinline__ void bin_trace_body(const PtPass &P) {
                     P.color[sid] = make_float4(c.x, c.y, c.z, 0.0f);
                 }
                 if constexpr (TAPS) P.rout[pos].q[2] = make_uint4(0u, 0u, sid, PT_AUX_MISS);
-                else PT_ST(P.hq + pos, make_uint4(0u, PT_AUX_MISS, 0u, slot), PT_NT_HQ_ON);
+                else P.hq[pos] = make_uint4(0u, PT_AUX_MISS, 0u, slot);
                 if constexpr (GEN) P.color[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // (no gen pass zeroed it)
             } else {
                 if constexpr (TAPS) {  // hit record: hit point + normal differences
                     store_ray(P.rout + pos, ro, rd, thr, rng, sid, uint32_t(mat),
                               make_uint4(__float_as_uint(dv0), __float_as_uint(dv1), __float_as_uint(dv2), 0u));
                 } else {  // hit quad: t, material, tap bound, slot (bin_shade_body)
-                    PT_ST(P.hq + pos,
-                          make_uint4(__float_as_uint(t), uint32_t(mat), __float_as_uint(dv0),
-                                     GEN && P.gen_norec ? uint32_t(ck.lo) : slot),
-                          PT_NT_HQ_ON);
+                    P.hq[pos] = make_uint4(__float_as_uint(t), uint32_t(mat), __float_as_uint(dv0),
+                                           GEN && P.gen_norec ? uint32_t(ck.lo) : slot);
                     if (wide_of<Map>(P))
                         P.hitn[pos] = make_float4(0.0f, 0.0f, __uint_as_float(uint32_t(ck.hi)),
                                                   __uint_as_float(uint32_t(ck.hi >> 32)));

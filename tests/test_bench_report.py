@@ -200,8 +200,7 @@ def test_measured_view_pmc_and_calibration(frame, tmp_path, monkeypatch):
     (tmp_path / "profiles" / "zz_pmc.json").write_text(json.dumps(pmc))
     import flop_calib
 
-    ev = {"march_steps": 3.0, "xform_union": 20.0, "shape_evals": 30.0, "culled": 5.0, "samples": 40.0,
-          "primary_box_tests": 10.0}
+    ev = {"march_steps": 3.0, "xform_union": 20.0, "shape_evals": 30.0, "culled": 5.0, "samples": 40.0}
     cal = {"configs": 24, "classes": {"trace": {"executed_flops_per_event": ev, "rms_rel_residual": 0.01,
                                                 "survey_weights": {k: 1.0 for k in ev}},
                                       "shade": {"executed_flops_per_event": {}, "survey_weights": {}}}}
