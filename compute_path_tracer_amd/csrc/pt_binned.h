@@ -36,9 +36,6 @@
 #define PT_BIN_NONE 0xffffffffu
 #define PT_AUX_MISS 0xffffffffu  // trace -> shade: PtRay q2.w of a position whose segment missed
 #define PT_BIN_BLOCK 256  // threads per block of the gen / bounds / scatter kernels
-#ifndef PT_SHADE_BLOCK
-#define PT_SHADE_BLOCK PT_BIN_BLOCK  // threads per block of the scene kernels' shade pass
-#endif
 // A pass's control words (PtPass.ctrl): [0] = its ray count, and the trace
 // pass's run cursors, one per share of the pass (PT_RUN_SHARDS, one per XCD),
 // each on its own 128-byte line.
@@ -441,9 +438,6 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
     // round trips after the taps
     constexpr int NM = MapMats<Map>::n;
     __shared__ PtMat lm[NM > 0 ? NM : 1];
-#ifdef PT_EMIT_PREFETCH
-    __shared__ float4 cpf[PT_SHADE_BLOCK];  // each lane's colour slot, loaded ahead (LDS DMA, base + lane x 16 B)
-#endif
     const PtMat *mats = P.L.mats;
     if constexpr (NM > 0) {
         const uint4 *src = reinterpret_cast<const uint4 *>(P.L.mats);
@@ -517,16 +511,7 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
         if (P.gen_trace) {  // first segment, no gen pass: the slot was never zeroed; 0 + e = e
             P.color[sid] = make_float4(ret.x, ret.y, ret.z, 0.0f);
         } else if (ret.x != 0.0f || ret.y != 0.0f || ret.z != 0.0f) {
-#ifdef PT_EMIT_PREFETCH
-            // (the slot, loaded into LDS before the taps; .w is always 0).  An
-            // explicit vmcnt(0) first: only the issuing wave's covering vmcnt
-            // orders a ds_read behind its LDS DMA, and an older hipRTC (the
-            // one a torch-first process binds to) emits none here
-            __builtin_amdgcn_s_waitcnt(0x0f70);
-            float4 c = cpf[threadIdx.x];
-#else
             float4 c = P.color[sid];
-#endif
             c.x += ret.x;
             c.y += ret.y;
             c.z += ret.z;
@@ -604,26 +589,6 @@ __device__ __forceinline__ void bin_shade_body(const PtPass &P) {
                 const float4 nd = P.hitn[i];
                 hi = make_uint2(__float_as_uint(nd.z), __float_as_uint(nd.w));
             }
-#ifdef PT_EMIT_PREFETCH
-            // (experiment) a hit on an emitting material will add to its
-            // sample's colour slot after the taps: the slot's load goes to
-            // LDS now (no registers held across the taps), so the add does
-            // not wait a memory round trip
-            // (the gathered ray first, on every path: the compiler waits for
-            // a load issued before a branch that may or may not issue the DMA
-            // with vmcnt(0), which would make the taps wait for the DMA too)
-            uint32_t z = 0u;  // (0, through an asm that takes the whole ray: the DMA's address depends on it)
-            __asm__ volatile("" : "+v"(z) : "v"(q0.x), "v"(q0.y), "v"(q0.z), "v"(q0.w), "v"(q1.x), "v"(q1.y),
-                             "v"(q1.z), "v"(q1.w), "v"(q2.x), "v"(q2.y), "v"(q2.z), "v"(q3.x), "v"(q3.y));
-            if (!P.gen_trace) {
-                const PtMat &em = mats[int(hq.y)];
-                if (em.emis[0] != 0.0f || em.emis[1] != 0.0f || em.emis[2] != 0.0f) {
-                    const uint32_t wv = uint32_t(__builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)));
-                    __builtin_amdgcn_global_load_lds(P.color + (q2.z + z),
-                                                     (__attribute__((address_space(3))) void *)(cpf + wv * 64u), 16, 0, 0);
-                }
-            }
-#endif
             shade_one(i, q0, q1, q2, q3, hi, hq);
         }
     }

@@ -38,7 +38,6 @@ struct PtJitModule {
     hipFunction_t gen = nullptr;  // camera rays + the scene's straight-line bounds()
     hipFunction_t gen_stats = nullptr;
     hipFunction_t trace_g = nullptr;  // first pass with its own camera rays (PtPass gen_trace)
-    int shade_block = 0;              // threads per block of shade_t / shade_t_stats (their launch bound)
     std::string key;  // generated source
 };
 

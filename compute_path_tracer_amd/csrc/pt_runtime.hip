@@ -968,10 +968,7 @@ static int launch_binned(pt_ctx *c, PtLaunch &L, bool stats) {
             if (!stats) HIPCHK(c, record_event(c->slog, c->lane[i].stream));
             if (taps_shade) {
                 void *args[] = {&S};
-                // (the same threads per CU whatever the build's block size)
-                const unsigned sb = unsigned(jm->shade_block > 0 ? jm->shade_block : PT_BIN_BLOCK);
-                const unsigned sg = std::max(1u, unsigned(size_t(shade_grid) * PT_BIN_BLOCK / sb));
-                HIPCHK(c, hipModuleLaunchKernel(stats ? jm->shade_t_stats : jm->shade_t, sg, 1, 1, sb,
+                HIPCHK(c, hipModuleLaunchKernel(stats ? jm->shade_t_stats : jm->shade_t, shade_grid, 1, 1, PT_BIN_BLOCK,
                                                 1, 1, 0, c->lane[i].stream, args, nullptr));
             } else {
                 pt_launch_bin(PtBinStage::Shade, S, stats, shade_grid, c->lane[i].stream);
@@ -1336,7 +1333,7 @@ int pt_get_option(pt_ctx *c, const char *key, double *value) {
         const PtJitModule *m = jit_active(c);
         const bool tr = key[4] == 't';
         const hipFunction_t f = m ? (tr ? m->trace_m : m->shade_t) : nullptr;
-        const int threads = tr ? 64 : (m && m->shade_block > 0 ? m->shade_block : PT_BIN_BLOCK);
+        const int threads = tr ? 64 : PT_BIN_BLOCK;
         int blocks = 0;
         if (f && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, threads, 0) != hipSuccess) blocks = 0;
         *value = double(blocks) * (threads / 64) / 4.0;  // (4 SIMDs per CU)
