@@ -478,6 +478,15 @@ def edit_slot(prog) -> int:
     raise ValueError("no shape")
 
 
+def edited_data(prog, ulps: int) -> tuple:
+    """(slot, data[]) with the edit_slot value moved `ulps` steps up the
+    float grid (away from zero)."""
+    k = edit_slot(prog)
+    edited = np.ascontiguousarray(prog.data, dtype=np.float32).copy()
+    edited[k:k + 1] = (edited[k:k + 1].view(np.int32) + np.int32(ulps)).view(np.float32)
+    return k, edited
+
+
 def value_edit_leg(pt, prog) -> dict:
     """What one value edit costs an editing session (outside the timed
     region).  The reference's edit is a buffer refresh
@@ -486,14 +495,16 @@ def value_edit_leg(pt, prog) -> dict:
     from the next dispatch on (table_kernel's throughput), and the
     values-baked build for the new values compiles on a worker thread
     (hipRTC; the edited values' source is in no cache) and replaces it when
-    it lands.  One Float (edit_slot) is nudged by one ulp; tier_up_s is the
+    it lands.  One Float (edit_slot) is nudged by a few ulps; tier_up_s is the
     wall time from pt_set_data until that build is installed (jit_wait),
     tier_compile_s the compile's own seconds.  Then the original values are
     restored (their baked build comes from the shipped cache)."""
     data = np.ascontiguousarray(prog.data, dtype=np.float32)
-    k = edit_slot(prog)
-    edited = data.copy()
-    edited[k] = np.nextafter(edited[k], np.float32(np.inf))
+    # a different small edit every run (1..4095 ulps): hipRTC / comgr keep a
+    # compile cache of their own, and an earlier run on the same box (the GPU
+    # tests run this leg too) must not have compiled the edited source
+    ulps = int(np.random.default_rng(time.time_ns() ^ os.getpid()).integers(1, 4096))
+    k, edited = edited_data(prog, ulps)
     pt.set_option("jit_bake", 2)
     t0 = time.perf_counter()
     pt.set_data(edited)
@@ -503,9 +514,10 @@ def value_edit_leg(pt, prog) -> dict:
     t2 = time.perf_counter()
     out = {"tier_up_s": round(t2 - t0, 3), "tier_compile_s": round(pt.get_option("jit_tier_seconds"), 3),
            "set_data_s": round(t1 - t0, 4), "table_kernel_meanwhile": on_table,
-           "tier_active_after": bool(pt.get_option("jit_tier_active")), "edited_slot": k,
-           "edit": "a shape size (data[edited_slot]) nudged by one ulp: no identity flag flips, so the table "
-                   "kernel is not rebuilt; the values-baked build is"}
+           "tier_active_after": bool(pt.get_option("jit_tier_active")), "edited_slot": k, "edit_ulps": ulps,
+           "edit": "a shape size (data[edited_slot]) nudged by edit_ulps ulps, a different edit every run (no "
+                   "compile cache has seen it); no identity flag flips, so the table kernel is not rebuilt; the "
+                   "values-baked build is"}
     pt.set_data(data)
     pt.set_option("jit_wait", 1)
     return out

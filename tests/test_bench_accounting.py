@@ -148,8 +148,9 @@ def test_value_edit_leg_rebuilds_only_the_baked_kernel(scene):
     from compute_path_tracer_amd.sdf_editor import CompData
 
     prog = scenes.SCENES[scene]().compile(CompData())
-    k = bench.edit_slot(prog)
-    edited = prog.data.astype(np.float32).copy()
-    edited[k] = np.nextafter(edited[k], np.float32(np.inf))
-    assert _kernel_source(prog, prog.data, 0) == _kernel_source(prog, edited, 0)
-    assert _kernel_source(prog, prog.data, 1) != _kernel_source(prog, edited, 1)
+    for ulps in (1, 4095):
+        k, edited = bench.edited_data(prog, ulps)
+        assert k == bench.edit_slot(prog) and edited[k] > prog.data[k]
+        assert np.count_nonzero(edited != prog.data) == 1
+        assert _kernel_source(prog, prog.data, 0) == _kernel_source(prog, edited, 0)
+        assert _kernel_source(prog, prog.data, 1) != _kernel_source(prog, edited, 1)
