@@ -117,6 +117,12 @@ def test_one_gpu_validate_and_tile_check(gpu):
     assert out["tile_check"]["bit_exact"] is True and out["tile_check"]["frames"] == 96
     assert out["roofline"]["kernel"] == "pt_bin_trace_m_jit"
     assert out["table_kernel"]["value"] > 0 and out["config"]["chunks_per_dispatch"] == 1.0
+    # the value edit: the table kernel renders at once,
+    # the values-baked rebuild of a never-seen edit compiles and lands
+    tk = out["table_kernel"]
+    assert tk["table_kernel_meanwhile"] is True and tk["tier_active_after"] is True
+    assert tk["tier_compile_s"] > 0.1 and tk["tier_up_s"] >= tk["tier_compile_s"] and 1 <= tk["edit_ulps"] < 4096
+    assert out["valid"] is True and out["schedule"]["bin_table"]["slots"] == 4096
 
 
 @pytest.mark.timeout(600)
