@@ -237,7 +237,9 @@ def calibrated_flops(cal: dict, cls: str, st: dict, taps: dict, n_aabb: int) -> 
     """(executed flops, {event: (count, executed flops, SURVEY-weight
     flops)}) of one kernel class over a dispatch's counters, at the
     calibration's fitted weights."""
-    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    sdir = os.path.join(ROOT, "scripts")
+    if sdir not in sys.path:
+        sys.path.insert(0, sdir)
     from flop_calib import features
 
     c = cal["classes"][cls]
