@@ -935,7 +935,18 @@ def main() -> None:
     # in the reduce); checked there against a fresh render of ~8 tiles, and
     # with --validate against a re-render of the whole image
     img = tr.image(0)
-    tile_check = None
+    # the boundary's one host transfer per render: the RGBA32F image read
+    # back (pt_read_accum, the reference's save_image copy, state.rs:243-263),
+    # timed alone after the steps; value_pcie_inclusive counts it once per step
+    readback = None
+    if world == 1:
+        rb = []
+        for _ in range(3):
+            pt.sync()
+            t1 = time.perf_counter()
+            pt.read_image()
+            rb.append(time.perf_counter() - t1)
+        readback = float(np.median(rb))
     validation = None
     if rank == 0:
         if not args.no_tile_check:
@@ -969,6 +980,14 @@ def main() -> None:
         out["render_ms_per_rank"] = render
         out["tile_check"] = tile_check
         out["schedule"]["bin_table"] = bin_table
+        if readback is not None:
+            out["host_readback"] = {
+                "bytes": int(width * height * 16), "ms": round(readback * 1e3, 3),
+                "gbs": round(width * height * 16 / readback / 1e9, 2),
+                "value_pcie_inclusive": round(samples_step * args.steps / (dt + args.steps * readback) / 1e6, 3),
+                "scope": "value with one image readback (pt_read_accum, RGBA32F) per step added; the headline "
+                         "value is device-resident (inputs in HBM, the image stays there, as the display pass "
+                         "reads it)"}
         if table is not None:
             out["table_kernel"] = table
     pt.close()
